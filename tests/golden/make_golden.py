@@ -1,0 +1,312 @@
+"""Generate the task-layer golden vectors from the reference's own modules.
+
+Run in the build container only (needs /root/reference; never runs on the GPU box):
+    python tests/golden/make_golden.py
+
+The reference env modules (mj_envs_vision/hand_manipulation_suite/*_v0.py) are imported with
+stub modules for the absent third-party packages (gym, mjrl, mujoco_py, cv2, torchvision;
+SURVEY §4.1).  Each env object is built with ``__new__`` and given a fake sim whose mjData
+arrays (qpos, qvel, body_xpos, body_xquat, site_xpos, sensordata) are synthetic, so
+``step()`` / ``get_obs()`` / ``reset_model()`` run the reference arithmetic exactly (fp64) on
+them.  ``do_simulation`` is stubbed to record the ctrl it receives (checks the action
+clip/scale of hammer_v0.py:55-59) and to leave the synthetic mjData in place.
+
+Outputs (data only, no reference source): tests/golden/task_<env>.npz, quatmath.npz,
+reset_<env>[_<variation>].npz.
+"""
+import importlib
+import os
+import sys
+import types
+
+import numpy as np
+
+REF = os.environ.get("ADROIT_REFERENCE", "/root/reference")
+OUT = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(OUT))
+sys.path.insert(0, REPO)
+
+
+def install_stubs():
+    def mod(name):
+        m = types.ModuleType(name)
+        sys.modules[name] = m
+        return m
+
+    gym = mod("gym")
+    gu = mod("gym.utils")
+
+    class EzPickle:
+        def __init__(self, *a, **k):
+            pass
+
+    gu.EzPickle = EzPickle
+    gym.utils = gu
+    reg = mod("gym.envs.registration")
+    reg.register = lambda **kw: None
+    envs = mod("gym.envs")
+    envs.registration = reg
+    gym.envs = envs
+    mjrl = mod("mjrl")
+    mjrl_envs = mod("mjrl.envs")
+    me = mod("mjrl.envs.mujoco_env")
+
+    class MujocoEnv:
+        def do_simulation(self, ctrl, n_frames):
+            self._ctrl_log.append((np.array(ctrl, dtype=np.float64).copy(), n_frames))
+
+        def set_state(self, qpos, qvel):
+            self.data.qpos[:] = qpos
+            self.data.qvel[:] = qvel
+
+    me.MujocoEnv = MujocoEnv
+    mjrl_envs.mujoco_env = me
+    mjrl.envs = mjrl_envs
+    mp = mod("mujoco_py")
+
+    class MjViewer:
+        def __init__(self, sim):
+            self.cam = types.SimpleNamespace(azimuth=0, distance=0, elevation=0)
+
+        def render(self):
+            pass
+
+    mp.MjViewer = MjViewer
+    mp.MjRenderContextOffscreen = object
+    mod("cv2")
+    tv = mod("torchvision")
+    tv.transforms = types.SimpleNamespace(Resize=lambda *a, **k: None, CenterCrop=lambda *a, **k: None)
+
+
+class FakeModel:
+    def __init__(self, m):
+        self._m = m
+        for f in ("body_pos", "body_quat", "site_pos", "body_mass", "geom_pos", "geom_size",
+                  "actuator_ctrlrange", "jnt_dofadr"):
+            setattr(self, f, np.array(getattr(m, f), dtype=np.float64 if f != "jnt_dofadr" else np.int64))
+        self.geom_rgba = np.ones((m.ngeom, 4))
+
+    def body_name2id(self, n):
+        return self._m.name2id("body", n)
+
+    def site_name2id(self, n):
+        return self._m.name2id("site", n)
+
+    def geom_name2id(self, n):
+        return self._m.name2id("geom", n)
+
+    def joint_name2id(self, n):
+        return self._m.name2id("joint", n)
+
+    def sensor_name2id(self, n):
+        return self._m.name2id("sensor", n)
+
+
+class FakeData:
+    def __init__(self, m):
+        self.qpos = np.zeros(m.nq)
+        self.qvel = np.zeros(m.nv)
+        self.body_xpos = np.zeros((m.nbody, 3))
+        self.body_xquat = np.tile([1.0, 0, 0, 0], (m.nbody, 1))
+        self.site_xpos = np.zeros((m.nsite, 3))
+        self.sensordata = np.zeros(m.nsensor)
+
+
+class FakeSim:
+    def __init__(self, model, data):
+        self.model = model
+        self.data = data
+
+    def reset(self):
+        self.data.qpos[:] = 0
+        self.data.qvel[:] = 0
+
+    def forward(self):
+        pass
+
+
+def make_env(mod, cls_name, env_id, model):
+    cls = getattr(mod, cls_name)
+    env = cls.__new__(cls)
+    fm, fd = FakeModel(model), FakeData(model)
+    env.sim = FakeSim(fm, fd)
+    env.model = fm
+    env.data = fd
+    env._ctrl_log = []
+    env.is_headless = False
+    env.observer = None
+    env.variation_type = None
+    cr = model.actuator_ctrlrange
+    env.act_mid = np.mean(cr, axis=1)
+    env.act_rng = 0.5 * (cr[:, 1] - cr[:, 0])
+    n = model.name2id
+    if env_id == "hammer-v0":
+        env.frame_skip = 5
+        env.target_obj_sid = n("site", "S_target")
+        env.S_grasp_sid = n("site", "S_grasp")
+        env.obj_bid = n("body", "Object")
+        env.tool_sid = n("site", "tool")
+        env.goal_sid = n("site", "nail_goal")
+    elif env_id == "door-v0":
+        env.frame_skip = 1
+        env.door_hinge_did = int(model.jnt_dofadr[n("joint", "door_hinge")])
+        env.grasp_sid = n("site", "S_grasp")
+        env.handle_sid = n("site", "S_handle")
+        env.door_bid = n("body", "frame")
+    elif env_id == "pen-v0":
+        from mj_envs_amd.tasks import pen_lengths
+        env.frame_skip = 5
+        env.target_obj_bid = n("body", "target")
+        env.S_grasp_sid = n("site", "S_grasp")
+        env.obj_bid = n("body", "Object")
+        env.eps_ball_sid = n("site", "eps_ball")
+        env.obj_t_sid = n("site", "object_top")
+        env.obj_b_sid = n("site", "object_bottom")
+        env.tar_t_sid = n("site", "target_top")
+        env.tar_b_sid = n("site", "target_bottom")
+        env.pen_length, env.tar_length = pen_lengths(model)
+    elif env_id == "relocate-v0":
+        env.frame_skip = 5
+        env.target_obj_sid = n("site", "target")
+        env.S_grasp_sid = n("site", "S_grasp")
+        env.obj_bid = n("body", "Object")
+    env.init_qpos = np.zeros(model.nq)
+    env.init_qvel = np.zeros(model.nv)
+    return env
+
+
+def random_quat(rng, k):
+    q = rng.normal(size=(k, 4))
+    return q / np.linalg.norm(q, axis=1, keepdims=True)
+
+
+def craft(env_id, model, rng, i, d):
+    """Push some samples onto the reward thresholds (bonus branches)."""
+    n = model.name2id
+    if env_id == "hammer-v0":
+        g, t = n("site", "nail_goal"), n("site", "S_target")
+        if i % 3 == 0:
+            d.site_xpos[t] = d.site_xpos[g] + rng.normal(scale=[0.004, 0.004, 0.004])
+        elif i % 3 == 1:
+            d.site_xpos[t] = d.site_xpos[g] + rng.normal(scale=[0.009, 0.009, 0.009])
+        d.body_xpos[n("body", "Object"), 2] = rng.uniform(0.0, 0.1)
+        d.site_xpos[n("site", "tool"), 2] = rng.uniform(0.0, 0.1)
+    elif env_id == "door-v0":
+        d.qpos[int(model.jnt_dofadr[n("joint", "door_hinge")])] = rng.uniform(-0.1, 1.6)
+    elif env_id == "pen-v0":
+        o, e = n("body", "Object"), n("site", "eps_ball")
+        d.body_xpos[o] = d.site_xpos[e] + rng.normal(scale=0.05, size=3)
+        d.body_xpos[o, 2] = rng.uniform(0.0, 0.3)
+        L = 0.065
+        tt, tb = n("site", "target_top"), n("site", "target_bottom")
+        ot, ob = n("site", "object_top"), n("site", "object_bottom")
+        c = rng.normal(size=3)
+        u = rng.normal(size=3)
+        u /= np.linalg.norm(u)
+        v = u + rng.normal(scale=[0.05, 0.3, 0.6][i % 3], size=3)
+        v /= np.linalg.norm(v)
+        d.site_xpos[tt], d.site_xpos[tb] = c + L * u, c - L * u
+        c2 = d.body_xpos[o]
+        d.site_xpos[ot], d.site_xpos[ob] = c2 + L * v, c2 - L * v
+    elif env_id == "relocate-v0":
+        o, tg = n("body", "Object"), n("site", "target")
+        d.body_xpos[o] = d.site_xpos[tg] + rng.normal(scale=[0.03, 0.07, 0.2][i % 3], size=3)
+        d.body_xpos[o, 2] = rng.uniform(0.0, 0.1) if i % 2 else d.body_xpos[o, 2]
+
+
+def gen_task(env_id, cls_name, module, nsamp=64):
+    from mj_envs_amd.tasks import load_model
+    model = load_model(env_id)
+    rng = np.random.default_rng(12345)
+    keys = ["qpos", "qvel", "xpos", "xquat", "site_xpos", "sensordata", "action", "ctrl", "obs",
+            "reward", "done", "goal", "obs_get"]
+    rec = {k: [] for k in keys}
+    for i in range(nsamp):
+        env = make_env(module, cls_name, env_id, model)
+        d = env.data
+        d.qpos[:] = rng.uniform(-1.5, 1.5, model.nq)
+        d.qvel[:] = rng.normal(scale=2.0, size=model.nv)
+        d.body_xpos[:] = rng.uniform(-0.5, 0.5, (model.nbody, 3))
+        d.body_xquat[:] = random_quat(rng, model.nbody)
+        if i % 8 == 7 and env_id == "hammer-v0":   # gimbal-lock branch of mat2euler (quatmath.py:84-95)
+            oid = model.name2id("body", "Object")
+            d.body_xquat[oid] = [np.cos(np.pi / 4), 0, np.sin(np.pi / 4) * (1 if i % 16 == 7 else -1), 0]
+        d.site_xpos[:] = rng.uniform(-0.5, 0.5, (model.nsite, 3))
+        d.sensordata[:] = rng.normal(scale=1.5, size=model.nsensor)
+        craft(env_id, model, rng, i, d)
+        a = rng.uniform(-1.3, 1.3, model.nu)
+        ob, r, done, info = env.step(a.copy())
+        ctrl, nfr = env._ctrl_log[-1]
+        rec["qpos"].append(d.qpos.copy()); rec["qvel"].append(d.qvel.copy())
+        rec["xpos"].append(d.body_xpos.copy()); rec["xquat"].append(d.body_xquat.copy())
+        rec["site_xpos"].append(d.site_xpos.copy()); rec["sensordata"].append(d.sensordata.copy())
+        rec["action"].append(a); rec["ctrl"].append(ctrl); rec["obs"].append(np.asarray(ob))
+        rec["reward"].append(float(r)); rec["done"].append(bool(done))
+        rec["goal"].append(bool(info["goal_achieved"])); rec["obs_get"].append(np.asarray(env.get_obs()))
+        assert nfr == env.frame_skip
+    out = {k: np.array(v) for k, v in rec.items()}
+    out["frame_skip"] = np.array(env.frame_skip)
+    if env_id == "pen-v0":
+        out["pen_length"] = np.array([env.pen_length, env.tar_length])
+    np.savez_compressed(os.path.join(OUT, f"task_{env_id.split('-')[0]}.npz"), **out)
+    print(env_id, {k: v.shape for k, v in out.items()},
+          "goals", int(out["goal"].sum()), "done", int(out["done"].sum()))
+
+
+def gen_reset(env_id, cls_name, module, variation=None, n=16, seed=777):
+    """Reset draws: run reset_model with a seeded Generator, record the written model fields."""
+    from mj_envs_amd.tasks import load_model, param_layout
+    model = load_model(env_id)
+    lay = param_layout(env_id, model, variation)
+    env = make_env(module, cls_name, env_id, model)
+    env.variation_type = variation
+    env.np_random = np.random.default_rng(seed)
+    vals = []
+    for _ in range(n):
+        env.reset_model()
+        row = []
+        for field, obj, comp in lay:
+            arr = getattr(env.model, field)
+            row.append(arr[obj] if arr.ndim == 1 else arr[obj, comp])
+        vals.append(row)
+    tag = env_id.split("-")[0] + (f"_{variation}" if variation else "")
+    np.savez_compressed(os.path.join(OUT, f"reset_{tag}.npz"), params=np.array(vals), seed=np.array(seed))
+    print("reset", tag, np.array(vals)[:2])
+
+
+def gen_quatmath():
+    sys.path.insert(0, os.path.join(REF, "mj_envs_vision", "utils"))
+    qm = importlib.import_module("quatmath")
+    rng = np.random.default_rng(4242)
+    q = rng.normal(size=(256, 4))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    special = np.array([[1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 1, 0], [0, 0, 0, 1],
+                        [np.cos(np.pi / 4), 0, np.sin(np.pi / 4), 0],
+                        [np.cos(np.pi / 4), 0, -np.sin(np.pi / 4), 0],
+                        [0.5, 0.5, 0.5, 0.5], [2.0, 0, 0, 0], [0, 0, 0, 0], [1e-9, 0, 0, 0]])
+    q = np.concatenate([q, special, 3.0 * q[:16]])
+    e = np.array([qm.quat2euler(x) for x in q])
+    eul = rng.uniform(-np.pi, np.pi, size=(256, 3))
+    eq = np.array([qm.euler2quat(x) for x in eul])
+    np.savez_compressed(os.path.join(OUT, "quatmath.npz"), quat=q, euler=e, euler_in=eul, quat_out=eq)
+    print("quatmath", q.shape, eul.shape)
+
+
+def main():
+    install_stubs()
+    sys.path.insert(0, REF)
+    gen_quatmath()
+    pkg = "mj_envs_vision.hand_manipulation_suite."
+    mods = {e: importlib.import_module(pkg + e.split("-")[0] + "_v0") for e in
+            ["hammer-v0", "door-v0", "pen-v0", "relocate-v0"]}
+    names = {"hammer-v0": "HammerEnvV0", "door-v0": "DoorEnvV0", "pen-v0": "PenEnvV0",
+             "relocate-v0": "RelocateEnvV0"}
+    for e in mods:
+        gen_task(e, names[e], mods[e])
+        gen_reset(e, names[e], mods[e])
+    for v in ("mass", "pos", "size"):
+        gen_reset("hammer-v0", "HammerEnvV0", mods["hammer-v0"], variation=v)
+
+
+if __name__ == "__main__":
+    main()
