@@ -1,0 +1,176 @@
+"""ctypes binding of the C-ABI in include/adroit_wave.h (libadroit_hip.so).
+
+The product path: every compute call goes to the HIP library.  There is no CPU fallback:
+if the library is missing or cannot be loaded, ``load()`` raises.  Device memory is managed
+with torch (``torch.cuda`` tensors are HIP allocations on ROCm); pointers and the current
+stream are passed through as plain integers.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libadroit_hip.so")
+
+AW_NDIMS = 13
+AW_DUMP_SIZE = 2728
+# float offsets inside the aw_forward_dump output (see adroit_wave.hip k_dump)
+DUMP_LAYOUT = dict(xpos=(0, 96), xquat=(96, 128), site_xpos=(224, 96), qacc_smooth=(320, 36),
+                   qfrc_smooth=(356, 36), qacc=(392, 36), qfrc_constraint=(428, 36), qM=(464, 1296),
+                   scalars=(1760, 8), con_dist=(1768, 32), con_pos=(1800, 96), con_frame=(1896, 288),
+                   con_pair=(2184, 32), efc_force=(2216, 128), efc_aref=(2344, 128), efc_D=(2472, 128),
+                   efc_type=(2600, 128))
+
+_lib = None
+_vp = ctypes.c_void_p
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libadroit_hip.so (raises if absent: the HIP path is the only path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(f"{LIB_PATH} not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    L.aw_last_error.restype = ctypes.c_char_p
+    L.aw_create.argtypes = [_vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_vp)]
+    L.aw_destroy.argtypes = [_vp]
+    L.aw_dims.argtypes = [_vp, ctypes.POINTER(ctypes.c_int)]
+    L.aw_set_option.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    L.aw_reset.argtypes = [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]
+    L.aw_step.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_uint64, _vp]
+    L.aw_random_actions.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp]
+    L.aw_get_state.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp]
+    L.aw_set_state.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.aw_status.argtypes = [_vp, _vp, _vp]
+    L.aw_episode_stats.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp]
+    L.aw_task_eval.argtypes = [_vp, ctypes.c_int] + [_vp] * 10 + [_vp]
+    L.aw_forward_dump.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp]
+    for f in ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "aw_step",
+              "aw_random_actions", "aw_get_state", "aw_set_state", "aw_status", "aw_episode_stats",
+              "aw_task_eval", "aw_forward_dump"):
+        getattr(L, f).restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+EXPORTS = ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "aw_step",
+           "aw_random_actions", "aw_get_state", "aw_set_state", "aw_status", "aw_episode_stats",
+           "aw_task_eval", "aw_forward_dump", "aw_last_error")
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise NativeError(f"adroit_wave error {rc}: {load().aw_last_error().decode()}")
+
+
+def _ptr(t) -> Optional[int]:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def _stream():
+    import torch
+    return torch.cuda.current_stream().cuda_stream
+
+
+class Sim:
+    """One batch of ``n_envs`` envs of one task on one GPU (owns the device state)."""
+
+    def __init__(self, blob: bytes, n_envs: int, device: int = 0):
+        import torch
+        L = load()
+        self.device = device
+        self.torch_device = torch.device("cuda", device)
+        self._blob = ctypes.create_string_buffer(blob, len(blob))
+        h = _vp()
+        with torch.cuda.device(device):
+            _check(L.aw_create(self._blob, len(blob), n_envs, device, ctypes.byref(h)))
+        self.h = h
+        d = (ctypes.c_int * AW_NDIMS)()
+        _check(L.aw_dims(self.h, d))
+        (self.nq, self.nv, self.nu, self.obs_dim, self.nparam, self.frame_skip, self.horizon,
+         self.task_kind, self.n_envs, self.nbody, self.nsite, self.ngeom, self.npair) = list(d)
+
+    def close(self):
+        if getattr(self, "h", None):
+            load().aw_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- buffers ---------------------------------------------------------------------------
+    def empty(self, *shape, dtype=None):
+        import torch
+        return torch.empty(*shape, dtype=dtype or torch.float32, device=self.torch_device)
+
+    def set_option(self, disableflags: int = -1, iterations: int = -1, noslip_iterations: int = -1):
+        _check(load().aw_set_option(self.h, disableflags, iterations, noslip_iterations))
+
+    def reset(self, obs, params=None, mask=None, seed: int = 1):
+        _check(load().aw_reset(self.h, _ptr(mask), _ptr(params), seed, _ptr(obs), _stream()))
+
+    def step(self, actions, obs, reward, done, goal, terminal_obs=None, autoreset: bool = False,
+             seed: int = 1):
+        _check(load().aw_step(self.h, _ptr(actions), _ptr(obs), _ptr(reward), _ptr(done), _ptr(goal),
+                              _ptr(terminal_obs), int(autoreset), seed, _stream()))
+
+    def random_actions(self, out, seed: int, step: int):
+        _check(load().aw_random_actions(self.h, seed, step, _ptr(out), _stream()))
+
+    def get_state(self, qpos=None, qvel=None, warm=None, params=None):
+        _check(load().aw_get_state(self.h, _ptr(qpos), _ptr(qvel), _ptr(warm), _ptr(params), _stream()))
+
+    def set_state(self, qpos=None, qvel=None, warm=None, params=None, obs=None):
+        _check(load().aw_set_state(self.h, _ptr(qpos), _ptr(qvel), _ptr(warm), _ptr(params), _ptr(obs),
+                                   _stream()))
+
+    def status(self, out):
+        _check(load().aw_status(self.h, _ptr(out), _stream()))
+
+    def episode_stats(self, last_return=None, last_goal=None, last_len=None, episodes=None):
+        _check(load().aw_episode_stats(self.h, _ptr(last_return), _ptr(last_goal), _ptr(last_len),
+                                       _ptr(episodes), _stream()))
+
+    def task_eval(self, n, qpos, qvel, xpos, xquat, site_xpos, touch, obs, reward, done, goal):
+        _check(load().aw_task_eval(self.h, n, _ptr(qpos), _ptr(qvel), _ptr(xpos), _ptr(xquat),
+                                   _ptr(site_xpos), _ptr(touch), _ptr(obs), _ptr(reward), _ptr(done),
+                                   _ptr(goal), _stream()))
+
+    def forward_dump(self, env: int, ctrl=None) -> dict:
+        import torch
+        out = self.empty(AW_DUMP_SIZE)
+        _check(load().aw_forward_dump(self.h, env, _ptr(ctrl), _ptr(out), _stream()))
+        o = out.cpu().numpy().astype(np.float64)
+        res = {k: o[a:a + n] for k, (a, n) in DUMP_LAYOUT.items()}
+        nv, nb, ns = self.nv, self.nbody, self.nsite
+        res["xpos"] = res["xpos"][:3 * nb].reshape(nb, 3)
+        res["xquat"] = res["xquat"][:4 * nb].reshape(nb, 4)
+        res["site_xpos"] = res["site_xpos"][:3 * ns].reshape(ns, 3)
+        for k in ("qacc_smooth", "qfrc_smooth", "qacc", "qfrc_constraint"):
+            res[k] = res[k][:nv]
+        res["qM"] = res["qM"][:nv * nv].reshape(nv, nv)
+        sc = res["scalars"]
+        ncon, nefc = int(sc[0]), int(sc[1])
+        res.update(ncon=ncon, nefc=nefc, nsparse=int(sc[2]), ndense=int(sc[3]), touch=sc[4], status=int(sc[5]))
+        res["con_dist"] = res["con_dist"][:ncon]
+        res["con_pos"] = res["con_pos"][:3 * ncon].reshape(ncon, 3)
+        res["con_frame"] = res["con_frame"][:9 * ncon].reshape(ncon, 9)
+        res["con_pair"] = res["con_pair"][:ncon].astype(int)
+        for k in ("efc_force", "efc_aref", "efc_D", "efc_type"):
+            res[k] = res[k][:nefc]
+        return res

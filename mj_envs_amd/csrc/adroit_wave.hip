@@ -1,0 +1,862 @@
+// adroit_wave.hip -- MI355X batched Adroit simulator: kernels + C-ABI (include/adroit_wave.h).
+//
+// One workgroup = one 64-lane wave = one env.  A step launch runs frame_skip x mj_step
+// (forward + Euler) and the task layer for every env; the per-env working set stays in LDS /
+// VGPRs for the whole launch, so HBM traffic is the compulsory state + action + obs bytes.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/adroit_wave.h"
+#include "../../include/aw_blob.h"
+#include "aw_collide.h"
+#include "aw_common.h"
+#include "aw_dynamics.h"
+#include "aw_solver.h"
+#include "aw_task.h"
+
+using namespace aw;
+
+// ---------------------------------------------------------------------------------------
+// device-side state owned by the handle
+struct DState {
+  float* qpos; float* qvel; float* warm; float* params;
+  int* ep_len; float* ep_ret; int* ep_goal; int* episode; unsigned* status;
+  float* last_ret; int* last_goal; int* last_len;
+};
+
+// ---------------------------------------------------------------------------------------
+// contacts -> key order (bitonic sort of (key, slot) over the wave), then frames
+__device__ void sort_contacts(Env& s, int lane) {
+  int n = s.ncon;
+  if (n > MAXCON) n = MAXCON;
+  int key = lane < n ? s.con_key[lane] : 0x7fffffff;
+  int idx = lane;
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      int pk = __shfl_xor(key, j, 64), pi = __shfl_xor(idx, j, 64);
+      bool up = (lane & k) == 0;
+      bool lower = (lane & j) == 0;
+      bool take = (lower == up) ? (pk < key) : (pk > key);
+      if (take) { key = pk; idx = pi; }
+    }
+  }
+  float dist = 0.f, pos[3] = {0, 0, 0}, nrm[3] = {0, 0, 0};
+  int pair = 0;
+  if (lane < n) {
+    dist = s.con_dist[idx];
+    pair = s.con_pair[idx];
+    for (int k = 0; k < 3; k++) { pos[k] = s.con_pos[idx][k]; nrm[k] = s.con_frame[idx][k]; }
+  }
+  wsync();
+  if (lane < n) {
+    s.con_key[lane] = key;
+    s.con_dist[lane] = dist;
+    s.con_pair[lane] = pair;
+    copy3(s.con_pos[lane], pos);
+    float f[9] = {nrm[0], nrm[1], nrm[2], 0, 0, 0, 0, 0, 0};
+    make_frame(f);
+    for (int k = 0; k < 9; k++) s.con_frame[lane][k] = f[k];
+  }
+  if (lane == 0) s.ncon = n;
+  wsync();
+}
+
+__device__ void stage_collision(const DModel& m, Env& s, int lane) {
+  if (lane == 0) s.ncon = 0;
+  wsync();
+  if (!(m.disableflags & (DSBL_CONSTRAINT | DSBL_CONTACT)))
+    for (int p = lane; p < m.npairall; p += 64) collide_pair(m, s, p);
+  wsync();
+  sort_contacts(s, lane);
+}
+
+// mj_forward: everything up to qacc / forces / sensors; Mrow is left in registers
+template <int NV>
+__device__ void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
+  stage_kinematics(m, s, lane);
+  stage_collision(m, s, lane);
+  stage_com(m, s, lane);
+  stage_crb<NV>(m, s, lane, Mrow);
+  stage_velocity(m, s, lane);
+  // qacc_smooth = M \ qfrc_smooth
+  {
+    float row[NV];
+#pragma unroll
+    for (int k = 0; k < NV; k++) row[k] = Mrow[k];
+    float invd = 1.f;
+    chol_factor<NV>(row, lane, invd);
+    chol_store<NV>(row, lane, s);
+    wsync();
+    float fs = lane < NV ? s.qfrc_smooth[lane] : 0.f;
+    float x = chol_solve<NV>(row, invd, fs, lane, s);
+    if (lane < NV) s.qacc_smooth[lane] = x;
+    wsync();
+  }
+  stage_constraints<NV>(m, s, lane);
+  if (s.nefc == 0) {
+    if (lane < NV) { s.qacc[lane] = s.qacc_smooth[lane]; s.qfrc_con[lane] = 0.f; }
+    wsync();
+  } else {
+    float a = 0.f;
+    solve_newton<NV>(m, s, lane, Mrow, a);
+    if (m.noslip_iterations > 0 && !(m.disableflags & DSBL_NOSLIP)) solve_noslip<NV>(m, s, lane, Mrow, a);
+    for (int r = lane; r < s.nefc; r += 64) s.rowbuf[r] = s.efc_force[r];
+    wsync();
+    float qc = jt_mul<NV>(s, lane);
+    if (lane < NV) { s.qacc[lane] = a; s.qfrc_con[lane] = qc; }
+    wsync();
+  }
+  stage_touch(m, s, lane);
+}
+
+// mj_Euler: implicit joint damping, semi-implicit positions, warmstart <- qacc
+template <int NV>
+__device__ void euler(const DModel& m, Env& s, int lane, const float (&Mrow)[NV]) {
+  const float h = m.timestep;
+  const bool dmp = !(m.disableflags & (DSBL_EULERDAMP | DSBL_PASSIVE));
+  float acc;
+  if (dmp) {
+    float row[NV];
+    const float dd = lane < NV ? h * m.dof_damping[lane] : 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; k++) row[k] = Mrow[k] + (k == lane ? dd : 0.f);
+    float invd = 1.f;
+    chol_factor<NV>(row, lane, invd);
+    chol_store<NV>(row, lane, s);
+    wsync();
+    float f = lane < NV ? s.qfrc_smooth[lane] + s.qfrc_con[lane] : 0.f;
+    acc = chol_solve<NV>(row, invd, f, lane, s);
+  } else {
+    acc = lane < NV ? s.qacc[lane] : 0.f;
+  }
+  if (lane < NV) {
+    float v = s.qvel[lane] + h * acc;
+    s.qvel[lane] = v;
+    s.qpos[lane] += h * v;
+    s.warm[lane] = s.qacc[lane];
+  }
+  wsync();
+}
+
+template <int NV>
+__device__ void reset_state(Env& s, int lane) {
+  if (lane < NV) { s.qpos[lane] = 0.f; s.qvel[lane] = 0.f; s.warm[lane] = 0.f; }
+  wsync();
+}
+
+__device__ __forceinline__ bool bad_value(float x) { return !(fabsf(x) <= 1e10f); }
+
+// mj_step (Euler) with mj_checkPos / checkVel / checkAcc
+template <int NV>
+__device__ void substep(const DModel& m, Env& s, int lane) {
+  float Mrow[NV];
+  {
+    bool bp = lane < NV && bad_value(s.qpos[lane]);
+    bool bv = lane < NV && bad_value(s.qvel[lane]);
+    unsigned long long bpm = __ballot(bp), bvm = __ballot(bv);
+    if (bpm | bvm) {
+      if (lane == 0) s.status |= (bpm ? ST_BADQPOS : 0u) | (bvm ? ST_BADQVEL : 0u);
+      reset_state<NV>(s, lane);
+    }
+  }
+  forward<NV>(m, s, lane, Mrow);
+  if (__ballot(lane < NV && bad_value(s.qacc[lane]))) {
+    if (lane == 0) s.status |= ST_BADQACC;
+    reset_state<NV>(s, lane);
+    forward<NV>(m, s, lane, Mrow);
+  }
+  euler<NV>(m, s, lane, Mrow);
+}
+
+// ---------------------------------------------------------------------------------------
+template <int NV>
+__device__ void load_env(const DModel& m, Env& s, const DState& st, int env, int lane) {
+  if (lane < NV) {
+    s.qpos[lane] = st.qpos[(size_t)env * m.nq + lane];
+    s.qvel[lane] = st.qvel[(size_t)env * m.nv + lane];
+    s.warm[lane] = st.warm[(size_t)env * m.nv + lane];
+  }
+  if (lane == 0) s.status = 0u;
+}
+template <int NV>
+__device__ void store_env(const DModel& m, Env& s, const DState& st, int env, int lane) {
+  if (lane < NV) {
+    st.qpos[(size_t)env * m.nq + lane] = s.qpos[lane];
+    st.qvel[(size_t)env * m.nv + lane] = s.qvel[lane];
+    st.warm[(size_t)env * m.nv + lane] = s.warm[lane];
+  }
+}
+__device__ void write_obs(const DModel& m, Env& s, int lane, float* out) {
+  task_obs(m, s, lane, s.rowbuf);
+  wsync();
+  for (int o = lane; o < m.obs_dim; o += 64) out[o] = s.rowbuf[o];
+  wsync();
+}
+
+// reset one env in LDS: params (given or sampled), qpos0/0/0, forward, obs
+template <int NV>
+__device__ void reset_env(const DModel& m, Env& s, const DState& st, int env, int lane,
+                          const float* params_in, uint64_t seed, float* obs) {
+  float* prm = st.params + (size_t)env * m.nparam;
+  if (lane == 0) {
+    if (params_in) {
+      for (int p = 0; p < m.nparam; p++) prm[p] = params_in[(size_t)env * m.nparam + p];
+    } else {
+      float tmp[MAXP];
+      sample_params(m, seed, (uint32_t)env, (uint32_t)st.episode[env], tmp);
+      for (int p = 0; p < m.nparam; p++) prm[p] = tmp[p];
+    }
+    st.ep_len[env] = 0;
+    st.ep_ret[env] = 0.f;
+    st.ep_goal[env] = 0;
+  }
+  __threadfence_block();
+  wsync();
+  if (lane < m.nu) s.ctrl[lane] = 0.f;
+  reset_state<NV>(s, lane);
+  stage_model(m, s, prm, lane);
+  float Mrow[NV];
+  forward<NV>(m, s, lane, Mrow);
+  if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
+}
+
+template <int NV>
+__global__ void __launch_bounds__(64) k_step(DModel m, DState st, int n, const float* __restrict__ actions,
+                                             float* obs, float* reward, uint8_t* done, uint8_t* goal,
+                                             float* terminal_obs, int autoreset, uint64_t seed) {
+  __shared__ Env s;
+  const int env = blockIdx.x, lane = threadIdx.x;
+  if (env >= n) return;
+  load_env<NV>(m, s, st, env, lane);
+  if (lane < m.nu) {
+    float a = clampf(actions[(size_t)env * m.nu + lane], -1.f, 1.f);
+    s.ctrl[lane] = m.act_mid[lane] + a * m.act_rng[lane];
+  }
+  stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
+  for (int k = 0; k < m.frame_skip; k++) substep<NV>(m, s, lane);
+  float* ob = obs + (size_t)env * m.obs_dim;
+  write_obs(m, s, lane, ob);
+  int term = 0, trunc = 0;
+  if (lane == 0) {
+    float r;
+    int dn, gl;
+    task_reward(m, s, &r, &dn, &gl);
+    reward[env] = r;
+    goal[env] = (uint8_t)gl;
+    int t = st.ep_len[env] + 1;
+    term = dn;
+    trunc = (m.horizon > 0 && t >= m.horizon) ? 1 : 0;
+    done[env] = (uint8_t)(term | (trunc << 1));
+    float ret = st.ep_ret[env] + r;
+    int gcount = st.ep_goal[env] + gl;
+    st.ep_len[env] = t;
+    st.ep_ret[env] = ret;
+    st.ep_goal[env] = gcount;
+    st.status[env] = s.status;
+    if (term || trunc) {
+      st.last_ret[env] = ret;
+      st.last_goal[env] = gcount;
+      st.last_len[env] = t;
+      st.episode[env] += 1;
+    }
+  }
+  store_env<NV>(m, s, st, env, lane);
+  int ended = __shfl(term | trunc, 0, 64);
+  if (autoreset && ended) {
+    __threadfence_block();
+    if (terminal_obs)
+      for (int o = lane; o < m.obs_dim; o += 64) terminal_obs[(size_t)env * m.obs_dim + o] = s.rowbuf[o];
+    wsync();
+    reset_env<NV>(m, s, st, env, lane, nullptr, seed, obs);
+    store_env<NV>(m, s, st, env, lane);
+  }
+}
+
+template <int NV>
+__global__ void __launch_bounds__(64) k_reset(DModel m, DState st, int n, const uint8_t* mask,
+                                              const float* params, uint64_t seed, float* obs) {
+  __shared__ Env s;
+  const int env = blockIdx.x, lane = threadIdx.x;
+  if (env >= n) return;
+  if (mask && !mask[env]) return;
+  if (lane == 0) s.status = 0u;
+  reset_env<NV>(m, s, st, env, lane, params, seed, obs);
+  store_env<NV>(m, s, st, env, lane);
+}
+
+template <int NV>
+__global__ void __launch_bounds__(64) k_set_state(DModel m, DState st, int n, const float* qpos,
+                                                  const float* qvel, const float* warm,
+                                                  const float* params, float* obs) {
+  __shared__ Env s;
+  const int env = blockIdx.x, lane = threadIdx.x;
+  if (env >= n) return;
+  load_env<NV>(m, s, st, env, lane);
+  if (lane < NV) {
+    if (qpos) s.qpos[lane] = qpos[(size_t)env * m.nq + lane];
+    if (qvel) s.qvel[lane] = qvel[(size_t)env * m.nv + lane];
+    if (warm) s.warm[lane] = warm[(size_t)env * m.nv + lane];
+  }
+  if (params && lane < m.nparam) st.params[(size_t)env * m.nparam + lane] = params[(size_t)env * m.nparam + lane];
+  __threadfence_block();
+  wsync();
+  if (lane < m.nu) s.ctrl[lane] = 0.f;
+  stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
+  float Mrow[NV];
+  forward<NV>(m, s, lane, Mrow);
+  if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
+  store_env<NV>(m, s, st, env, lane);
+}
+
+// dump layout (floats): see mj_envs_amd/_native.py DUMP_LAYOUT
+template <int NV>
+__global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const float* ctrl, float* out) {
+  __shared__ Env s;
+  const int lane = threadIdx.x;
+  load_env<NV>(m, s, st, env, lane);
+  if (lane < m.nu) s.ctrl[lane] = ctrl ? ctrl[lane] : 0.f;
+  stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
+  float Mrow[NV];
+  forward<NV>(m, s, lane, Mrow);
+  for (int i = lane; i < MAXB * 3; i += 64) out[i] = i < m.nbody * 3 ? (&s.xpos[0][0])[i] : 0.f;
+  for (int i = lane; i < MAXB * 4; i += 64) out[96 + i] = i < m.nbody * 4 ? (&s.xquat[0][0])[i] : 0.f;
+  for (int i = lane; i < MAXS * 3; i += 64) out[224 + i] = i < m.nsite * 3 ? (&s.sxpos[0][0])[i] : 0.f;
+  if (lane < MAXV) {
+    bool v = lane < NV;
+    out[320 + lane] = v ? s.qacc_smooth[lane] : 0.f;
+    out[356 + lane] = v ? s.qfrc_smooth[lane] : 0.f;
+    out[392 + lane] = v ? s.qacc[lane] : 0.f;
+    out[428 + lane] = v ? s.qfrc_con[lane] : 0.f;
+  }
+  for (int k = 0; k < NV; k++)
+    if (lane < NV) out[464 + lane * NV + k] = Mrow[k];
+  if (lane == 0) {
+    out[1760] = (float)s.ncon; out[1761] = (float)s.nefc; out[1762] = (float)s.nsparse;
+    out[1763] = (float)s.ndense; out[1764] = s.touch[0]; out[1765] = (float)s.status;
+  }
+  if (lane < MAXCON) {
+    bool v = lane < s.ncon;
+    out[1768 + lane] = v ? s.con_dist[lane] : 0.f;
+    for (int k = 0; k < 3; k++) out[1800 + 3 * lane + k] = v ? s.con_pos[lane][k] : 0.f;
+    for (int k = 0; k < 9; k++) out[1896 + 9 * lane + k] = v ? s.con_frame[lane][k] : 0.f;
+    out[2184 + lane] = v ? (float)s.con_pair[lane] : -1.f;
+  }
+  for (int r = lane; r < MAXEFC; r += 64) {
+    bool v = r < s.nefc;
+    out[2216 + r] = v ? s.efc_force[r] : 0.f;
+    out[2344 + r] = v ? s.efc_aref[r] : 0.f;
+    out[2472 + r] = v ? s.efc_D[r] : 0.f;
+    out[2600 + r] = v ? (float)s.efc_type[r] : -1.f;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_task_eval(DModel m, int n, const float* qpos, const float* qvel,
+                                                  const float* xpos, const float* xquat, const float* sxpos,
+                                                  const float* touch, float* obs, float* reward, uint8_t* done,
+                                                  uint8_t* goal) {
+  __shared__ Env s;
+  const int i = blockIdx.x, lane = threadIdx.x;
+  if (i >= n) return;
+  if (lane < m.nq) s.qpos[lane] = qpos[(size_t)i * m.nq + lane];
+  if (lane < m.nv) s.qvel[lane] = qvel[(size_t)i * m.nv + lane];
+  for (int k = lane; k < m.nbody * 3; k += 64) (&s.xpos[0][0])[k] = xpos[(size_t)i * m.nbody * 3 + k];
+  for (int k = lane; k < m.nbody * 4; k += 64) (&s.xquat[0][0])[k] = xquat[(size_t)i * m.nbody * 4 + k];
+  for (int k = lane; k < m.nsite * 3; k += 64) (&s.sxpos[0][0])[k] = sxpos[(size_t)i * m.nsite * 3 + k];
+  if (lane == 0) s.touch[0] = touch ? touch[i] : 0.f;
+  wsync();
+  write_obs(m, s, lane, obs + (size_t)i * m.obs_dim);
+  if (lane == 0) {
+    float r;
+    int dn, gl;
+    task_reward(m, s, &r, &dn, &gl);
+    reward[i] = r; done[i] = (uint8_t)dn; goal[i] = (uint8_t)gl;
+  }
+}
+
+__global__ void k_random_actions(int n, int nu, uint64_t seed, uint64_t step, float* out) {
+  int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= n) return;
+  for (int blk = 0; blk * 4 < nu; blk++) {
+    uint32_t c[4] = {(uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), (uint32_t)blk};
+    philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    for (int k = 0; k < 4 && blk * 4 + k < nu; k++) out[(size_t)env * nu + blk * 4 + k] = 2.f * u01(c[k]) - 1.f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// host side
+namespace {
+thread_local std::string g_err;
+int fail(int code, const std::string& msg) { g_err = msg; return code; }
+#define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return fail(AW_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); } while (0)
+
+struct Blob {
+  const void* p; size_t n;
+  bool has(const char* name) const { aw_blob_entry e; return aw_blob_find(p, n, name, &e); }
+  std::vector<double> f(const char* name) const {
+    aw_blob_entry e;
+    std::vector<double> out;
+    if (!aw_blob_find(p, n, name, &e)) return out;
+    size_t cnt = (size_t)e.rows * e.cols;
+    out.resize(cnt);
+    const char* d = (const char*)e.data;
+    for (size_t i = 0; i < cnt; i++) {
+      if (e.kind == 0) { double v; memcpy(&v, d + 8 * i, 8); out[i] = v; }
+      else { int32_t v; memcpy(&v, d + 4 * i, 4); out[i] = v; }
+    }
+    return out;
+  }
+  std::vector<int> i(const char* name) const {
+    std::vector<double> v = f(name);
+    return std::vector<int>(v.begin(), v.end());
+  }
+  int dim(const char* name, int dflt = -1) const { return aw_blob_dim(p, n, name, dflt); }
+  double opt(const char* name, double dflt) const { return aw_blob_opt(p, n, name, dflt); }
+};
+
+struct Packer {
+  std::vector<char> buf;
+  std::vector<std::pair<size_t, const void**>> fix;
+  template <class T>
+  void add(const T** slot, const std::vector<T>& v) {
+    size_t off = (buf.size() + 15) & ~size_t(15);
+    buf.resize(off + std::max<size_t>(v.size(), 1) * sizeof(T), 0);
+    if (!v.empty()) memcpy(buf.data() + off, v.data(), v.size() * sizeof(T));
+    fix.push_back({off, (const void**)slot});
+  }
+};
+
+std::vector<float> tof(const std::vector<double>& v) { return std::vector<float>(v.begin(), v.end()); }
+}  // namespace
+
+struct aw_handle {
+  int device, nenv, NV;
+  DModel m;
+  DState st;
+  void* dmodel = nullptr;
+  void* dstate = nullptr;
+};
+
+static int build_model(const Blob& B, DModel& m, Packer& P) {
+  memset(&m, 0, sizeof(m));
+  int nq = B.dim("nq"), nv = B.dim("nv"), nu = B.dim("nu"), nbody = B.dim("nbody"), njnt = B.dim("njnt");
+  int ngeom_all = B.dim("ngeom"), nsite = B.dim("nsite"), ntendon = B.dim("ntendon");
+  int npair = B.dim("npair"), ncand = B.dim("ncand"), nsensor = B.dim("nsensor");
+  if (nq < 0 || nv < 0 || nbody < 0 || B.dim("task_kind") < 0) return fail(AW_EBLOB, "model table lacks dims / task block");
+  if (nq != nv || njnt != nv) return fail(AW_EUNSUPPORTED, "only hinge/slide joints are supported");
+  if (nv > MAXV || nbody > MAXB || nsite > MAXS || ntendon > MAXT || nu > MAXU)
+    return fail(AW_EUNSUPPORTED, "model exceeds kernel capacity");
+  m.nq = nq; m.nv = nv; m.nu = nu; m.nbody = nbody; m.njnt = njnt; m.nsite = nsite; m.ntendon = ntendon;
+  m.timestep = (float)B.opt("timestep", 0.002);
+  m.gravity[0] = (float)B.opt("gravity_x", 0); m.gravity[1] = (float)B.opt("gravity_y", 0);
+  m.gravity[2] = (float)B.opt("gravity_z", -9.81);
+  m.iterations = (int)B.opt("iterations", 100);
+  m.tolerance = (float)B.opt("tolerance", 1e-8);
+  m.noslip_iterations = (int)B.opt("noslip_iterations", 0);
+  m.noslip_tolerance = (float)B.opt("noslip_tolerance", 1e-6);
+  m.mpr_tolerance = (float)B.opt("mpr_tolerance", 1e-6);
+  m.mpr_iterations = (int)B.opt("mpr_iterations", 50);
+  m.meaninertia = (float)B.opt("meaninertia", 1);
+  m.pen_length = (float)B.opt("task_pen_length", 1);
+  m.tar_length = (float)B.opt("task_tar_length", 1);
+  m.task_kind = B.dim("task_kind"); m.frame_skip = B.dim("task_frame_skip", 1);
+  m.horizon = B.dim("task_horizon", 0); m.obs_dim = B.dim("task_obs_dim", 0);
+  m.nparam = B.dim("task_nparam", 0); m.variation = B.dim("task_variation", 0);
+  if (m.nparam > MAXP) return fail(AW_EUNSUPPORTED, "too many per-env params");
+  m.disableflags = 0;
+
+  std::vector<int> parent = B.i("body_parentid"), rootid = B.i("body_rootid"), dofnum = B.i("body_dofnum"),
+                   dofadr = B.i("body_dofadr");
+  // subtree ends (DFS order), levels, dof masks
+  std::vector<int> send(nbody), depth(nbody, 0);
+  for (int b = 0; b < nbody; b++) send[b] = b + 1;
+  for (int b = nbody - 1; b > 0; b--) send[parent[b]] = std::max(send[parent[b]], send[b]);
+  for (int b = 1; b < nbody; b++) depth[b] = depth[parent[b]] + 1;
+  int nlev = 0;
+  for (int b = 0; b < nbody; b++) nlev = std::max(nlev, depth[b] + 1);
+  if (nlev > MAXLEV) return fail(AW_EUNSUPPORTED, "tree too deep");
+  std::vector<int> lstart(nlev + 1, 0), lbody;
+  for (int l = 0; l < nlev; l++) {
+    lstart[l] = (int)lbody.size();
+    for (int b = 0; b < nbody; b++)
+      if (depth[b] == l) lbody.push_back(b);
+  }
+  lstart[nlev] = (int)lbody.size();
+  m.nlevel = nlev;
+  std::vector<int> dparent = B.i("dof_parentid");
+  std::vector<unsigned long long> bmask(nbody, 0), amask(nv, 0);
+  for (int b = 1; b < nbody; b++) {
+    int a = b;
+    while (a > 0) {
+      for (int k = 0; k < dofnum[a]; k++) bmask[b] |= 1ull << (dofadr[a] + k);
+      a = parent[a];
+    }
+  }
+  for (int j = 0; j < nv; j++)
+    for (int a = dparent[j]; a >= 0; a = dparent[a]) amask[j] |= 1ull << a;
+
+  P.add(&m.body_parentid, parent); P.add(&m.body_rootid, rootid); P.add(&m.body_dofnum, dofnum);
+  P.add(&m.body_dofadr, dofadr); P.add(&m.body_subtree_end, send); P.add(&m.level_start, lstart);
+  P.add(&m.level_body, lbody);
+  P.add(&m.body_pos, tof(B.f("body_pos"))); P.add(&m.body_quat, tof(B.f("body_quat")));
+  P.add(&m.body_ipos, tof(B.f("body_ipos"))); P.add(&m.body_iquat, tof(B.f("body_iquat")));
+  P.add(&m.body_mass, tof(B.f("body_mass"))); P.add(&m.body_inertia, tof(B.f("body_inertia")));
+  P.add(&m.body_invweight0, tof(B.f("body_invweight0")));
+  P.add(&m.body_subtreemass, tof(B.f("body_subtreemass")));
+  P.add(&m.body_dofmask, bmask);
+
+  std::vector<int> jtype = B.i("jnt_type");
+  for (int t : jtype) if (t != JNT_HINGE && t != JNT_SLIDE) return fail(AW_EUNSUPPORTED, "joint type");
+  P.add(&m.jnt_type, jtype); P.add(&m.jnt_bodyid, B.i("jnt_bodyid")); P.add(&m.jnt_limited, B.i("jnt_limited"));
+  P.add(&m.jnt_pos, tof(B.f("jnt_pos"))); P.add(&m.jnt_axis, tof(B.f("jnt_axis")));
+  P.add(&m.jnt_range, tof(B.f("jnt_range"))); P.add(&m.jnt_margin, tof(B.f("jnt_margin")));
+  P.add(&m.jnt_solref, tof(B.f("jnt_solref"))); P.add(&m.jnt_solimp, tof(B.f("jnt_solimp")));
+
+  // actuators (joint transmission, one per dof)
+  std::vector<int> trn = B.i("actuator_trnid");
+  std::vector<int> dact(nv, -1);
+  for (int u = 0; u < nu; u++) {
+    if (dact[trn[u]] >= 0) return fail(AW_EUNSUPPORTED, "two actuators on one joint");
+    dact[trn[u]] = u;
+  }
+  std::vector<double> floss = B.f("dof_frictionloss");
+  std::vector<int> fl_dof, fl_row(nv, -1);
+  for (int j = 0; j < nv; j++)
+    if (floss[j] > 0) { fl_row[j] = (int)fl_dof.size(); fl_dof.push_back(j); }
+  m.nfl = (int)fl_dof.size();
+  P.add(&m.dof_bodyid, B.i("dof_bodyid")); P.add(&m.dof_act, dact); P.add(&m.fl_dof, fl_dof);
+  P.add(&m.fl_row, fl_row); P.add(&m.dof_ancmask, amask);
+  P.add(&m.dof_armature, tof(B.f("dof_armature"))); P.add(&m.dof_damping, tof(B.f("dof_damping")));
+  P.add(&m.dof_frictionloss, tof(floss)); P.add(&m.dof_invweight0, tof(B.f("dof_invweight0")));
+  P.add(&m.dof_solref, tof(B.f("dof_solref"))); P.add(&m.dof_solimp, tof(B.f("dof_solimp")));
+
+  // compact collidable geoms
+  std::vector<int> gtype = B.i("geom_type"), gcon = B.i("geom_contype"), gaff = B.i("geom_conaffinity"),
+                   gbody = B.i("geom_bodyid");
+  std::vector<double> gpos = B.f("geom_pos"), gquat = B.f("geom_quat"), gsize = B.f("geom_size"),
+                      grb = B.f("geom_rbound");
+  std::vector<int> gmap(ngeom_all, -1), ctype, cbody;
+  std::vector<float> cpos, cquat, csize, crb;
+  for (int g = 0; g < ngeom_all; g++) {
+    if (gtype[g] == 7 || (gcon[g] == 0 && gaff[g] == 0)) continue;
+    gmap[g] = (int)ctype.size();
+    ctype.push_back(gtype[g]); cbody.push_back(gbody[g]);
+    for (int k = 0; k < 3; k++) { cpos.push_back((float)gpos[3 * g + k]); csize.push_back((float)gsize[3 * g + k]); }
+    for (int k = 0; k < 4; k++) cquat.push_back((float)gquat[4 * g + k]);
+    crb.push_back((float)grb[g]);
+  }
+  m.ngeom = (int)ctype.size();
+  if (m.ngeom > MAXG) return fail(AW_EUNSUPPORTED, "too many collidable geoms");
+  P.add(&m.geom_type, ctype); P.add(&m.geom_bodyid, cbody); P.add(&m.geom_pos, cpos);
+  P.add(&m.geom_quat, cquat); P.add(&m.geom_size, csize); P.add(&m.geom_rbound, crb);
+
+  P.add(&m.site_bodyid, B.i("site_bodyid")); P.add(&m.site_pos, tof(B.f("site_pos")));
+  P.add(&m.site_quat, tof(B.f("site_quat")));
+
+  // tendons: fixed, <= 2 joints
+  std::vector<int> tadr = B.i("tendon_adr"), tnum = B.i("tendon_num"), wj = B.i("wrap_jnt");
+  std::vector<double> wc = B.f("wrap_coef"), tfl = B.f("tendon_frictionloss");
+  std::vector<int> d0(ntendon), d1(ntendon);
+  std::vector<float> c0(ntendon), c1(ntendon);
+  for (int t = 0; t < ntendon; t++) {
+    if (tnum[t] < 1 || tnum[t] > 2) return fail(AW_EUNSUPPORTED, "tendon with != 1..2 joints");
+    if (tfl[t] > 0) return fail(AW_EUNSUPPORTED, "tendon frictionloss");
+    d0[t] = wj[tadr[t]]; c0[t] = (float)wc[tadr[t]];
+    d1[t] = tnum[t] > 1 ? wj[tadr[t] + 1] : -1; c1[t] = tnum[t] > 1 ? (float)wc[tadr[t] + 1] : 0.f;
+  }
+  P.add(&m.ten_d0, d0); P.add(&m.ten_d1, d1); P.add(&m.ten_limited, B.i("tendon_limited"));
+  P.add(&m.ten_c0, c0); P.add(&m.ten_c1, c1); P.add(&m.ten_range, tof(B.f("tendon_range")));
+  P.add(&m.ten_margin, tof(B.f("tendon_margin"))); P.add(&m.ten_solref, tof(B.f("tendon_solref")));
+  P.add(&m.ten_solimp, tof(B.f("tendon_solimp"))); P.add(&m.ten_invweight0, tof(B.f("tendon_invweight0")));
+
+  std::vector<double> gain = B.f("actuator_gainprm");
+  std::vector<float> g0(nu);
+  for (int u = 0; u < nu; u++) g0[u] = (float)gain[3 * u];
+  P.add(&m.act_ctrllimited, B.i("actuator_ctrllimited")); P.add(&m.act_forcelimited, B.i("actuator_forcelimited"));
+  P.add(&m.act_gear, tof(B.f("actuator_gear"))); P.add(&m.act_gain, g0);
+  P.add(&m.act_bias, tof(B.f("actuator_biasprm"))); P.add(&m.act_ctrlrange, tof(B.f("actuator_ctrlrange")));
+  P.add(&m.act_forcerange, tof(B.f("actuator_forcerange")));
+
+  // unified pair list: explicit pairs (own params), then candidates (params mixed here in fp64,
+  // mj_contactParam with equal priorities)
+  std::vector<int> pg1, pg2, pcd;
+  std::vector<float> pfr, psr, psi, pmg, pgp;
+  {
+    std::vector<int> e1 = B.i("pair_geom1"), e2 = B.i("pair_geom2"), ecd = B.i("pair_condim");
+    std::vector<double> efr = B.f("pair_friction"), esr = B.f("pair_solref"), esi = B.f("pair_solimp"),
+                        emg = B.f("pair_margin"), egp = B.f("pair_gap");
+    for (int p = 0; p < npair; p++) {
+      if (gmap[e1[p]] < 0 || gmap[e2[p]] < 0) return fail(AW_EUNSUPPORTED, "pair with a visual geom");
+      pg1.push_back(gmap[e1[p]]); pg2.push_back(gmap[e2[p]]); pcd.push_back(ecd[p]);
+      for (int k = 0; k < 5; k++) pfr.push_back((float)efr[5 * p + k]);
+      for (int k = 0; k < 2; k++) psr.push_back((float)esr[2 * p + k]);
+      for (int k = 0; k < 5; k++) psi.push_back((float)esi[5 * p + k]);
+      pmg.push_back((float)emg[p]); pgp.push_back((float)egp[p]);
+    }
+    std::vector<int> c1v = B.i("cand_geom1"), c2v = B.i("cand_geom2"), gcd = B.i("geom_condim");
+    std::vector<double> gfr = B.f("geom_friction"), gsm = B.f("geom_solmix"), gsr = B.f("geom_solref"),
+                        gsi = B.f("geom_solimp"), gmg = B.f("geom_margin"), ggp = B.f("geom_gap");
+    for (int c = 0; c < ncand; c++) {
+      int a = c1v[c], b = c2v[c];
+      pg1.push_back(gmap[a]); pg2.push_back(gmap[b]);
+      pcd.push_back(std::max(gcd[a], gcd[b]));
+      double s1 = gsm[a], s2 = gsm[b], mix;
+      if (s1 >= 1e-15 && s2 >= 1e-15) mix = s1 / (s1 + s2);
+      else if (s1 < 1e-15 && s2 < 1e-15) mix = 0.5;
+      else mix = s1 < 1e-15 ? 0.0 : 1.0;
+      double f0 = std::max(gfr[3 * a], gfr[3 * b]), f1 = std::max(gfr[3 * a + 1], gfr[3 * b + 1]),
+             f2 = std::max(gfr[3 * a + 2], gfr[3 * b + 2]);
+      double fr[5] = {f0, f0, f1, f2, f2};
+      for (int k = 0; k < 5; k++) pfr.push_back((float)fr[k]);
+      for (int k = 0; k < 2; k++) psr.push_back((float)(mix * gsr[2 * a + k] + (1 - mix) * gsr[2 * b + k]));
+      for (int k = 0; k < 5; k++) psi.push_back((float)(mix * gsi[5 * a + k] + (1 - mix) * gsi[5 * b + k]));
+      pmg.push_back((float)std::max(gmg[a], gmg[b])); pgp.push_back((float)std::max(ggp[a], ggp[b]));
+    }
+  }
+  m.npairall = (int)pg1.size();
+  P.add(&m.cp_g1, pg1); P.add(&m.cp_g2, pg2); P.add(&m.cp_condim, pcd); P.add(&m.cp_friction, pfr);
+  P.add(&m.cp_solref, psr); P.add(&m.cp_solimp, psi); P.add(&m.cp_margin, pmg); P.add(&m.cp_gap, pgp);
+
+  // task block
+  std::vector<int> tidx = B.i("task_idx"), pf = B.i("task_param_field"), po = B.i("task_param_obj"),
+                   pc = B.i("task_param_comp");
+  for (int p = 0; p < m.nparam; p++)
+    if (pf[p] == 4 || pf[p] == 5) {
+      if (gmap[po[p]] < 0) return fail(AW_EUNSUPPORTED, "param on a visual geom");
+      po[p] = gmap[po[p]];
+    }
+  // touch sensors read by the task (hammer: S_nail, task_idx[5] = its sensordata address)
+  std::vector<int> ts, ttype;
+  std::vector<float> tsize;
+  if (m.task_kind == 0 && tidx.size() > 5) {
+    std::vector<int> stype = B.i("sensor_type"), sobj = B.i("sensor_objid"), sadr = B.i("sensor_adr");
+    std::vector<int> sitetype = B.i("site_type");
+    std::vector<double> ssize = B.f("site_size");
+    for (int k = 0; k < nsensor; k++)
+      if (sadr[k] == tidx[5] && stype[k] == 0) {
+        ts.push_back(sobj[k]); ttype.push_back(sitetype[sobj[k]]);
+        for (int q = 0; q < 3; q++) tsize.push_back((float)ssize[3 * sobj[k] + q]);
+      }
+  }
+  m.ntouch = (int)ts.size();
+  P.add(&m.touch_site, ts); P.add(&m.touch_adr, ts); P.add(&m.touch_type, ttype); P.add(&m.touch_size, tsize);
+  P.add(&m.task_idx, tidx); P.add(&m.param_field, pf); P.add(&m.param_obj, po); P.add(&m.param_comp, pc);
+  P.add(&m.act_mid, tof(B.f("task_act_mid"))); P.add(&m.act_rng, tof(B.f("task_act_rng")));
+  P.add(&m.param_default, tof(B.f("task_param_default")));
+  std::vector<double> dlo = B.f("task_draw_lo"), dhi = B.f("task_draw_hi");
+  m.ndraw = (int)dlo.size();
+  if (m.ndraw > 8) return fail(AW_EUNSUPPORTED, "too many reset draws");
+  P.add(&m.draw_lo, tof(dlo)); P.add(&m.draw_hi, tof(dhi));
+  return AW_OK;
+}
+
+template <int NV>
+static void launch_step(aw_handle* h, const float* a, float* obs, float* rew, uint8_t* done, uint8_t* goal,
+                        float* tobs, int autoreset, uint64_t seed, hipStream_t st) {
+  hipLaunchKernelGGL((k_step<NV>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, a, obs, rew, done,
+                     goal, tobs, autoreset, seed);
+}
+template <int NV>
+static void launch_reset(aw_handle* h, const uint8_t* mask, const float* params, uint64_t seed, float* obs,
+                         hipStream_t st) {
+  hipLaunchKernelGGL((k_reset<NV>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, mask, params, seed, obs);
+}
+template <int NV>
+static void launch_set(aw_handle* h, const float* q, const float* v, const float* w, const float* p, float* obs,
+                       hipStream_t st) {
+  hipLaunchKernelGGL((k_set_state<NV>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, q, v, w, p, obs);
+}
+template <int NV>
+static void launch_dump(aw_handle* h, int env, const float* ctrl, float* out, hipStream_t st) {
+  hipLaunchKernelGGL((k_dump<NV>), dim3(1), dim3(64), 0, st, h->m, h->st, env, ctrl, out);
+}
+
+#define DISPATCH_NV(NVV, CALL)                                                     \
+  switch (NVV) {                                                                   \
+    case 30: CALL(30); break;                                                      \
+    case 33: CALL(33); break;                                                      \
+    case 36: CALL(36); break;                                                      \
+    default: return fail(AW_EUNSUPPORTED, "nv not instantiated (30/33/36)");      \
+  }
+
+extern "C" {
+
+const char* aw_last_error(void) { return g_err.c_str(); }
+
+int aw_create(const void* blob, size_t nbytes, int n_envs, int device, aw_handle** out) {
+  if (!blob || !out || n_envs <= 0) return fail(AW_EINVAL, "aw_create: bad arguments");
+  Blob B{blob, nbytes};
+  aw_handle* h = new aw_handle();
+  h->device = device;
+  h->nenv = n_envs;
+  Packer P;
+  int rc = build_model(B, h->m, P);
+  if (rc) { delete h; return rc; }
+  h->NV = h->m.nv;
+  if (h->NV != 30 && h->NV != 33 && h->NV != 36) { delete h; return fail(AW_EUNSUPPORTED, "nv not instantiated"); }
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipMalloc(&h->dmodel, P.buf.size()));
+  HIPCHK(hipMemcpy(h->dmodel, P.buf.data(), P.buf.size(), hipMemcpyHostToDevice));
+  for (auto& f : P.fix) *f.second = (const char*)h->dmodel + f.first;
+  // state
+  size_t N = (size_t)n_envs, nq = h->m.nq, nv = h->m.nv, np = std::max(h->m.nparam, 1);
+  size_t bytes = N * (nq + 2 * nv + np) * 4 + N * 4 * 10 + 256;
+  HIPCHK(hipMalloc(&h->dstate, bytes));
+  HIPCHK(hipMemset(h->dstate, 0, bytes));
+  char* p = (char*)h->dstate;
+  auto take = [&](size_t b) { char* r = p; p += (b + 255) & ~size_t(255); return r; };
+  h->st.qpos = (float*)take(N * nq * 4); h->st.qvel = (float*)take(N * nv * 4); h->st.warm = (float*)take(N * nv * 4);
+  h->st.params = (float*)take(N * np * 4); h->st.ep_len = (int*)take(N * 4); h->st.ep_ret = (float*)take(N * 4);
+  h->st.ep_goal = (int*)take(N * 4); h->st.episode = (int*)take(N * 4); h->st.status = (unsigned*)take(N * 4);
+  h->st.last_ret = (float*)take(N * 4); h->st.last_goal = (int*)take(N * 4); h->st.last_len = (int*)take(N * 4);
+  if ((size_t)(p - (char*)h->dstate) > bytes) {
+    // re-allocate with the exact size (alignment padding)
+    size_t need = (size_t)(p - (char*)h->dstate);
+    HIPCHK(hipFree(h->dstate));
+    HIPCHK(hipMalloc(&h->dstate, need));
+    HIPCHK(hipMemset(h->dstate, 0, need));
+    p = (char*)h->dstate;
+    h->st.qpos = (float*)take(N * nq * 4); h->st.qvel = (float*)take(N * nv * 4); h->st.warm = (float*)take(N * nv * 4);
+    h->st.params = (float*)take(N * np * 4); h->st.ep_len = (int*)take(N * 4); h->st.ep_ret = (float*)take(N * 4);
+    h->st.ep_goal = (int*)take(N * 4); h->st.episode = (int*)take(N * 4); h->st.status = (unsigned*)take(N * 4);
+    h->st.last_ret = (float*)take(N * 4); h->st.last_goal = (int*)take(N * 4); h->st.last_len = (int*)take(N * 4);
+  }
+  // default params for every env
+  std::vector<float> prm(N * np, 0.f);
+  std::vector<double> def = B.f("task_param_default");
+  for (size_t e = 0; e < N; e++)
+    for (int k = 0; k < h->m.nparam; k++) prm[e * np + k] = (float)def[k];
+  HIPCHK(hipMemcpy(h->st.params, prm.data(), prm.size() * 4, hipMemcpyHostToDevice));
+  *out = h;
+  return AW_OK;
+}
+
+int aw_destroy(aw_handle* h) {
+  if (!h) return AW_OK;
+  hipSetDevice(h->device);
+  if (h->dmodel) hipFree(h->dmodel);
+  if (h->dstate) hipFree(h->dstate);
+  delete h;
+  return AW_OK;
+}
+
+int aw_dims(const aw_handle* h, int* d) {
+  if (!h || !d) return fail(AW_EINVAL, "aw_dims: null");
+  const DModel& m = h->m;
+  int v[AW_NDIMS] = {m.nq, m.nv, m.nu, m.obs_dim, m.nparam, m.frame_skip, m.horizon, m.task_kind, h->nenv,
+                     m.nbody, m.nsite, m.ngeom, m.npairall};
+  memcpy(d, v, sizeof(v));
+  return AW_OK;
+}
+
+int aw_set_option(aw_handle* h, int disableflags, int iterations, int noslip_iterations) {
+  if (!h) return fail(AW_EINVAL, "aw_set_option: null");
+  if (disableflags >= 0) h->m.disableflags = disableflags;
+  if (iterations >= 0) h->m.iterations = iterations;
+  if (noslip_iterations >= 0) h->m.noslip_iterations = noslip_iterations;
+  return AW_OK;
+}
+
+int aw_reset(aw_handle* h, const uint8_t* mask, const float* params, uint64_t seed, float* obs, void* stream) {
+  if (!h) return fail(AW_EINVAL, "aw_reset: null");
+  HIPCHK(hipSetDevice(h->device));
+#define CALL(NVV) launch_reset<NVV>(h, mask, params, seed, obs, (hipStream_t)stream)
+  DISPATCH_NV(h->NV, CALL)
+#undef CALL
+  HIPCHK(hipGetLastError());
+  return AW_OK;
+}
+
+int aw_step(aw_handle* h, const float* actions, float* obs, float* reward, uint8_t* done, uint8_t* goal,
+            float* terminal_obs, int autoreset, uint64_t seed, void* stream) {
+  if (!h || !actions || !obs || !reward || !done || !goal) return fail(AW_EINVAL, "aw_step: null buffer");
+  HIPCHK(hipSetDevice(h->device));
+#define CALL(NVV) launch_step<NVV>(h, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, (hipStream_t)stream)
+  DISPATCH_NV(h->NV, CALL)
+#undef CALL
+  HIPCHK(hipGetLastError());
+  return AW_OK;
+}
+
+int aw_random_actions(aw_handle* h, uint64_t seed, uint64_t step, float* actions, void* stream) {
+  if (!h || !actions) return fail(AW_EINVAL, "aw_random_actions: null");
+  HIPCHK(hipSetDevice(h->device));
+  int bs = 256, nb = (h->nenv + bs - 1) / bs;
+  hipLaunchKernelGGL(k_random_actions, dim3(nb), dim3(bs), 0, (hipStream_t)stream, h->nenv, h->m.nu, seed, step, actions);
+  HIPCHK(hipGetLastError());
+  return AW_OK;
+}
+
+int aw_get_state(aw_handle* h, float* qpos, float* qvel, float* warm, float* params, void* stream) {
+  if (!h) return fail(AW_EINVAL, "aw_get_state: null");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  size_t N = h->nenv;
+  if (qpos) HIPCHK(hipMemcpyAsync(qpos, h->st.qpos, N * h->m.nq * 4, hipMemcpyDeviceToDevice, st));
+  if (qvel) HIPCHK(hipMemcpyAsync(qvel, h->st.qvel, N * h->m.nv * 4, hipMemcpyDeviceToDevice, st));
+  if (warm) HIPCHK(hipMemcpyAsync(warm, h->st.warm, N * h->m.nv * 4, hipMemcpyDeviceToDevice, st));
+  if (params && h->m.nparam)
+    HIPCHK(hipMemcpyAsync(params, h->st.params, N * h->m.nparam * 4, hipMemcpyDeviceToDevice, st));
+  return AW_OK;
+}
+
+int aw_set_state(aw_handle* h, const float* qpos, const float* qvel, const float* warm, const float* params,
+                 float* obs, void* stream) {
+  if (!h) return fail(AW_EINVAL, "aw_set_state: null");
+  HIPCHK(hipSetDevice(h->device));
+#define CALL(NVV) launch_set<NVV>(h, qpos, qvel, warm, params, obs, (hipStream_t)stream)
+  DISPATCH_NV(h->NV, CALL)
+#undef CALL
+  HIPCHK(hipGetLastError());
+  return AW_OK;
+}
+
+int aw_status(aw_handle* h, uint32_t* flags, void* stream) {
+  if (!h || !flags) return fail(AW_EINVAL, "aw_status: null");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipMemcpyAsync(flags, h->st.status, (size_t)h->nenv * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return AW_OK;
+}
+
+int aw_episode_stats(aw_handle* h, float* last_return, int32_t* last_goal, int32_t* last_len, int32_t* episodes,
+                     void* stream) {
+  if (!h) return fail(AW_EINVAL, "aw_episode_stats: null");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  size_t b = (size_t)h->nenv * 4;
+  if (last_return) HIPCHK(hipMemcpyAsync(last_return, h->st.last_ret, b, hipMemcpyDeviceToDevice, st));
+  if (last_goal) HIPCHK(hipMemcpyAsync(last_goal, h->st.last_goal, b, hipMemcpyDeviceToDevice, st));
+  if (last_len) HIPCHK(hipMemcpyAsync(last_len, h->st.last_len, b, hipMemcpyDeviceToDevice, st));
+  if (episodes) HIPCHK(hipMemcpyAsync(episodes, h->st.episode, b, hipMemcpyDeviceToDevice, st));
+  return AW_OK;
+}
+
+int aw_task_eval(aw_handle* h, int n, const float* qpos, const float* qvel, const float* xpos, const float* xquat,
+                 const float* sxpos, const float* touch, float* obs, float* reward, uint8_t* done, uint8_t* goal,
+                 void* stream) {
+  if (!h || n <= 0) return fail(AW_EINVAL, "aw_task_eval: bad arguments");
+  HIPCHK(hipSetDevice(h->device));
+  hipLaunchKernelGGL(k_task_eval, dim3(n), dim3(64), 0, (hipStream_t)stream, h->m, n, qpos, qvel, xpos, xquat,
+                     sxpos, touch, obs, reward, done, goal);
+  HIPCHK(hipGetLastError());
+  return AW_OK;
+}
+
+int aw_forward_dump(aw_handle* h, int env, const float* ctrl, float* out, void* stream) {
+  if (!h || !out || env < 0 || env >= h->nenv) return fail(AW_EINVAL, "aw_forward_dump: bad arguments");
+  HIPCHK(hipSetDevice(h->device));
+#define CALL(NVV) launch_dump<NVV>(h, env, ctrl, out, (hipStream_t)stream)
+  DISPATCH_NV(h->NV, CALL)
+#undef CALL
+  HIPCHK(hipGetLastError());
+  return AW_OK;
+}
+
+}  // extern "C"

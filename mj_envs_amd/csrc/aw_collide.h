@@ -1,0 +1,685 @@
+// aw_collide.h -- lane-per-pair narrowphase (fp32) for the Adroit primitive set.
+//
+// Restates MuJoCo 2.1 mj_collision (see oracle/collide.cc for the fp64 statement of the same
+// algorithms): bounding-sphere test (rbound + margin, planes exempt), analytic plane/sphere/
+// capsule/box colliders, SAT + fixed-order candidate points for box-box, libccd MPR (as used by
+// mjc_Convex) for every pair involving a cylinder.  Each lane owns one geom pair and appends
+// its contacts to the env's LDS list through an LDS atomic counter; the list is then sorted by
+// (pair index, emission index) so contact order -- and hence constraint row order -- is the
+// oracle's order.
+#pragma once
+#include "aw_common.h"
+
+namespace aw {
+
+struct GV {
+  float pos[3];
+  float mat[9];
+  float size[3];
+  int type;
+};
+
+struct Emit {
+  Env* s;
+  int pair;
+  int cnt;
+};
+
+__device__ __forceinline__ void axis_of(float* a, const float* m, int k) { a[0] = m[k]; a[1] = m[3 + k]; a[2] = m[6 + k]; }
+
+__device__ __forceinline__ void emit(Emit& e, float dist, const float* pos, const float* n) {
+  if (e.cnt >= MAXPAIRCON) return;
+  int slot = atomicAdd(&e.s->ncon, 1);
+  if (slot < MAXCON) {
+    e.s->con_key[slot] = e.pair * MAXPAIRCON + e.cnt;
+    e.s->con_pair[slot] = e.pair;
+    e.s->con_dist[slot] = dist;
+    copy3(e.s->con_pos[slot], pos);
+    float* f = e.s->con_frame[slot];
+    f[0] = n[0]; f[1] = n[1]; f[2] = n[2];
+    f[3] = f[4] = f[5] = 0.f;
+  } else {
+    atomicOr(&e.s->status, (unsigned)ST_CON_OVERFLOW);
+  }
+  e.cnt++;
+}
+
+// ---------------------------------------------------------------------------------------
+__device__ void c_plane_sphere(const float* p1, const float* m1, const float* p2, float r, float margin, Emit& e) {
+  float n[3], dif[3];
+  axis_of(n, m1, 2);
+  sub3(dif, p2, p1);
+  float dist = dot3(n, dif) - r;
+  if (dist > margin) return;
+  float pos[3];
+  for (int k = 0; k < 3; k++) pos[k] = p2[k] - n[k] * (r + dist / 2);
+  emit(e, dist, pos, n);
+}
+
+__device__ void c_plane_capsule(const GV& a, const GV& b, float margin, Emit& e) {
+  float ax[3], p[3];
+  axis_of(ax, b.mat, 2);
+  for (int s = 1; s >= -1; s -= 2) {
+    for (int k = 0; k < 3; k++) p[k] = b.pos[k] + s * ax[k] * b.size[1];
+    c_plane_sphere(a.pos, a.mat, p, b.size[0], margin, e);
+  }
+}
+
+__device__ void c_plane_box(const GV& a, const GV& b, float margin, Emit& e) {
+  float n[3], dif[3];
+  axis_of(n, a.mat, 2);
+  sub3(dif, b.pos, a.pos);
+  float dist = dot3(n, dif);
+  int cnt = 0;
+  for (int i = 0; i < 8; i++) {
+    float v[3] = {(i & 1) ? b.size[0] : -b.size[0], (i & 2) ? b.size[1] : -b.size[1], (i & 4) ? b.size[2] : -b.size[2]};
+    float corner[3];
+    mulmv3(corner, b.mat, v);
+    float ld = dot3(n, corner);
+    if (dist + ld > margin || ld > 0) continue;
+    float dd = dist + ld, pos[3];
+    for (int k = 0; k < 3; k++) pos[k] = corner[k] + b.pos[k] - n[k] * dd / 2;
+    emit(e, dd, pos, n);
+    if (++cnt >= 4) return;
+  }
+}
+
+__device__ void c_plane_cylinder(const GV& a, const GV& b, float margin, Emit& e) {
+  float n[3], axis[3], dif[3], vec[3];
+  axis_of(n, a.mat, 2);
+  axis_of(axis, b.mat, 2);
+  sub3(dif, b.pos, a.pos);
+  float dist0 = dot3(dif, n);
+  float prjaxis = dot3(n, axis);
+  if (prjaxis > 0) { scl3(axis, axis, -1); prjaxis = -prjaxis; }
+  for (int k = 0; k < 3; k++) vec[k] = axis[k] * prjaxis - n[k];
+  float len = norm3(vec);
+  if (len < MINVAL) axis_of(vec, b.mat, 0);
+  else scl3(vec, vec, 1.0f / len);
+  float r = b.size[0], h = b.size[1];
+  scl3(vec, vec, r);
+  float prjvec = dot3(vec, n);
+  float ah[3];
+  scl3(ah, axis, h);
+  float pa = prjaxis * h;
+  float pos[3], d;
+  d = dist0 + pa + prjvec;
+  if (d <= margin) {
+    for (int k = 0; k < 3; k++) pos[k] = b.pos[k] + ah[k] + vec[k] - n[k] * d / 2;
+    emit(e, d, pos, n);
+  }
+  d = dist0 - pa + prjvec;
+  if (d <= margin) {
+    for (int k = 0; k < 3; k++) pos[k] = b.pos[k] - ah[k] + vec[k] - n[k] * d / 2;
+    emit(e, d, pos, n);
+  }
+  d = dist0 + pa - prjvec / 2;
+  if (d <= margin) {
+    float v1[3];
+    cross3(v1, vec, axis);
+    scl3(v1, v1, 0.86602540378443864676f);
+    for (int s = -1; s <= 1; s += 2) {
+      for (int k = 0; k < 3; k++) pos[k] = b.pos[k] + ah[k] - vec[k] / 2 + s * v1[k] - n[k] * d / 2;
+      emit(e, d, pos, n);
+    }
+  }
+}
+
+__device__ void c_sphere_sphere(const float* p1, float r1, const float* p2, float r2, float margin, Emit& e) {
+  float dif[3];
+  sub3(dif, p2, p1);
+  float cd = norm3(dif);
+  float dist = cd - r1 - r2;
+  if (dist > margin) return;
+  float n[3] = {1, 0, 0};
+  if (cd > MINVAL) scl3(n, dif, 1.0f / cd);
+  float pos[3];
+  for (int k = 0; k < 3; k++) pos[k] = p1[k] + n[k] * (r1 + dist / 2);
+  emit(e, dist, pos, n);
+}
+
+__device__ void c_sphere_capsule(const GV& a, const GV& b, float margin, Emit& e) {
+  float ax[3], dif[3], q[3];
+  axis_of(ax, b.mat, 2);
+  sub3(dif, a.pos, b.pos);
+  float t = clampf(dot3(dif, ax), -b.size[1], b.size[1]);
+  for (int k = 0; k < 3; k++) q[k] = b.pos[k] + ax[k] * t;
+  c_sphere_sphere(a.pos, a.size[0], q, b.size[0], margin, e);
+}
+
+__device__ void seg_seg(const float* p1, const float* d1, const float* p2, const float* d2, float* c1, float* c2) {
+  float r[3];
+  sub3(r, p1, p2);
+  float a = dot3(d1, d1), ee = dot3(d2, d2), f = dot3(d2, r);
+  float s, t;
+  if (a <= MINVAL && ee <= MINVAL) { s = t = 0; }
+  else if (a <= MINVAL) { s = 0; t = clampf(f / ee, 0.f, 1.f); }
+  else {
+    float cc = dot3(d1, r);
+    if (ee <= MINVAL) { t = 0; s = clampf(-cc / a, 0.f, 1.f); }
+    else {
+      float b = dot3(d1, d2), den = a * ee - b * b;
+      s = den > MINVAL ? clampf((b * f - cc * ee) / den, 0.f, 1.f) : 0.f;
+      t = (b * s + f) / ee;
+      if (t < 0) { t = 0; s = clampf(-cc / a, 0.f, 1.f); }
+      else if (t > 1) { t = 1; s = clampf((b - cc) / a, 0.f, 1.f); }
+    }
+  }
+  for (int k = 0; k < 3; k++) { c1[k] = p1[k] + d1[k] * s; c2[k] = p2[k] + d2[k] * t; }
+}
+
+__device__ void c_capsule_capsule(const GV& a, const GV& b, float margin, Emit& e) {
+  float a1[3], a2[3], s1[3], s2[3], d1[3], d2[3], c1[3], c2[3];
+  axis_of(a1, a.mat, 2);
+  axis_of(a2, b.mat, 2);
+  for (int k = 0; k < 3; k++) {
+    s1[k] = a.pos[k] - a1[k] * a.size[1]; d1[k] = 2 * a1[k] * a.size[1];
+    s2[k] = b.pos[k] - a2[k] * b.size[1]; d2[k] = 2 * a2[k] * b.size[1];
+  }
+  seg_seg(s1, d1, s2, d2, c1, c2);
+  c_sphere_sphere(c1, a.size[0], c2, b.size[0], margin, e);
+}
+
+__device__ void c_sphere_box_pt(const float* p, float r, const GV& b, float margin, Emit& e) {
+  float dif[3], loc[3], cl[3];
+  sub3(dif, p, b.pos);
+  mulmtv3(loc, b.mat, dif);
+  bool inside = true;
+  for (int k = 0; k < 3; k++) {
+    cl[k] = clampf(loc[k], -b.size[k], b.size[k]);
+    if (fabsf(loc[k]) > b.size[k]) inside = false;
+  }
+  float n[3], dist;
+  if (!inside) {
+    float dl[3], dw[3];
+    sub3(dl, cl, loc);
+    float dd = norm3(dl);
+    dist = dd - r;
+    if (dist > margin) return;
+    mulmv3(dw, b.mat, dl);
+    scl3(n, dw, 1.0f / dd);
+  } else {
+    int kmin = 0;
+    float pen = b.size[0] - fabsf(loc[0]);
+    for (int k = 1; k < 3; k++) {
+      float pk = b.size[k] - fabsf(loc[k]);
+      if (pk < pen) { pen = pk; kmin = k; }
+    }
+    float nl[3] = {0, 0, 0};
+    nl[kmin] = loc[kmin] >= 0 ? -1.0f : 1.0f;
+    mulmv3(n, b.mat, nl);
+    dist = -pen - r;
+  }
+  float pos[3];
+  for (int k = 0; k < 3; k++) pos[k] = p[k] + n[k] * (r + dist / 2);
+  emit(e, dist, pos, n);
+}
+
+__device__ float box_sdist(const float* p, const GV& b) {
+  float dif[3], loc[3];
+  sub3(dif, p, b.pos);
+  mulmtv3(loc, b.mat, dif);
+  float out = 0, mx = -1e30f;
+  for (int k = 0; k < 3; k++) {
+    float q = fabsf(loc[k]) - b.size[k];
+    float qp = q > 0 ? q : 0;
+    out += qp * qp;
+    mx = fmaxf(mx, q);
+  }
+  return sqrtf(out) + (mx < 0 ? mx : 0);
+}
+
+__device__ void c_capsule_box(const GV& a, const GV& b, float margin, Emit& e) {
+  float ax[3], p[3];
+  axis_of(ax, a.mat, 2);
+  float h = a.size[1], r = a.size[0];
+  const float gr = 0.6180339887498949f;
+  float lo = -h, hi = h;
+  float x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo);
+  for (int k = 0; k < 3; k++) p[k] = a.pos[k] + ax[k] * x1;
+  float f1 = box_sdist(p, b);
+  for (int k = 0; k < 3; k++) p[k] = a.pos[k] + ax[k] * x2;
+  float f2 = box_sdist(p, b);
+  for (int it = 0; it < 40; it++) {
+    if (f1 < f2) {
+      hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
+      for (int k = 0; k < 3; k++) p[k] = a.pos[k] + ax[k] * x1;
+      f1 = box_sdist(p, b);
+    } else {
+      lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
+      for (int k = 0; k < 3; k++) p[k] = a.pos[k] + ax[k] * x2;
+      f2 = box_sdist(p, b);
+    }
+  }
+  float ts = 0.5f * (lo + hi);
+  for (int k = 0; k < 3; k++) p[k] = a.pos[k] + ax[k] * ts;
+  int before = e.cnt;
+  c_sphere_box_pt(p, r, b, margin, e);
+  if (e.cnt == before) return;
+  float te = ts > 0 ? -h : h;
+  if (fabsf(te - ts) > 1e-6f * (h + 1e-12f)) {
+    for (int k = 0; k < 3; k++) p[k] = a.pos[k] + ax[k] * te;
+    c_sphere_box_pt(p, r, b, margin, e);
+  }
+}
+
+__device__ void c_box_box(const GV& A, const GV& B, float margin, Emit& e) {
+  float a[3][3], b[3][3], t[3];
+  for (int k = 0; k < 3; k++) { axis_of(a[k], A.mat, k); axis_of(b[k], B.mat, k); }
+  sub3(t, B.pos, A.pos);
+  float best = -1e30f, bestn[3] = {0, 0, 0};
+  int bestk = -1;
+  for (int k = 0; k < 15; k++) {
+    float L[3];
+    if (k < 3) copy3(L, a[k]);
+    else if (k < 6) copy3(L, b[k - 3]);
+    else {
+      cross3(L, a[(k - 6) / 3], b[(k - 6) % 3]);
+      float ln = norm3(L);
+      if (ln < 1e-6f) continue;
+      scl3(L, L, 1.0f / ln);
+    }
+    float ra = A.size[0] * fabsf(dot3(L, a[0])) + A.size[1] * fabsf(dot3(L, a[1])) + A.size[2] * fabsf(dot3(L, a[2]));
+    float rb = B.size[0] * fabsf(dot3(L, b[0])) + B.size[1] * fabsf(dot3(L, b[1])) + B.size[2] * fabsf(dot3(L, b[2]));
+    float tl = dot3(t, L);
+    float sep = fabsf(tl) - ra - rb;
+    if (sep > margin) return;
+    float bias = k < 6 ? 0.f : 1e-6f;
+    if (sep > best + bias) {
+      best = sep; bestk = k;
+      copy3(bestn, L);
+      if (tl < 0) scl3(bestn, bestn, -1);
+    }
+  }
+  if (bestk < 0) return;
+  if (bestk < 6) {
+    const bool refA = bestk < 3;
+    const GV& R = refA ? A : B;
+    const GV& I = refA ? B : A;
+    float ra[3][3], ia[3][3];
+    for (int k = 0; k < 3; k++) {
+      copy3(ra[k], refA ? a[k] : b[k]);
+      copy3(ia[k], refA ? b[k] : a[k]);
+    }
+    int fk = refA ? bestk : bestk - 3;
+    float nr[3];
+    copy3(nr, bestn);
+    if (!refA) scl3(nr, nr, -1);
+    float sg = dot3(nr, ra[fk]) > 0 ? 1.f : -1.f;
+    int ru = (fk + 1) % 3, rv = (fk + 2) % 3;
+    float hu = R.size[ru], hv = R.size[rv];
+    float fc[3];
+    for (int k = 0; k < 3; k++) fc[k] = R.pos[k] + ra[fk][k] * sg * R.size[fk];
+    int ik = 0;
+    float imin = 1e30f, isg = 1;
+    for (int k = 0; k < 3; k++) {
+      float dd = dot3(ia[k], nr);
+      if (dd < imin) { imin = dd; ik = k; isg = 1; }
+      if (-dd < imin) { imin = -dd; ik = k; isg = -1; }
+    }
+    int iu = (ik + 1) % 3, iv = (ik + 2) % 3;
+    float inn[3], ic[3];
+    scl3(inn, ia[ik], isg);
+    for (int k = 0; k < 3; k++) ic[k] = I.pos[k] + inn[k] * I.size[ik];
+    float su = I.size[iu], sv = I.size[iv];
+    float P[4][3], pu[4], pv[4];
+    const float cs[4][2] = {{1, 1}, {-1, 1}, {-1, -1}, {1, -1}};
+    for (int q = 0; q < 4; q++) {
+      for (int k = 0; k < 3; k++) P[q][k] = ic[k] + ia[iu][k] * cs[q][0] * su + ia[iv][k] * cs[q][1] * sv;
+      float dv[3];
+      sub3(dv, P[q], fc);
+      pu[q] = dot3(dv, ra[ru]);
+      pv[q] = dot3(dv, ra[rv]);
+    }
+    auto em = [&](const float* p) {
+      float dv[3];
+      sub3(dv, p, fc);
+      float dist = dot3(dv, nr);
+      if (dist > margin) return;
+      float pos[3];
+      for (int k = 0; k < 3; k++) pos[k] = p[k] - nr[k] * dist / 2;
+      emit(e, dist, pos, bestn);
+    };
+    for (int q = 0; q < 4; q++)
+      if (fabsf(pu[q]) <= hu && fabsf(pv[q]) <= hv) em(P[q]);
+    float den = dot3(nr, inn);
+    if (fabsf(den) > 1e-12f) {
+      for (int q = 0; q < 4; q++) {
+        float Q[3], dq[3], Qp[3];
+        for (int k = 0; k < 3; k++) Q[k] = fc[k] + ra[ru][k] * cs[q][0] * hu + ra[rv][k] * cs[q][1] * hv;
+        sub3(dq, ic, Q);
+        float tt = dot3(dq, inn) / den;
+        for (int k = 0; k < 3; k++) Qp[k] = Q[k] + nr[k] * tt;
+        sub3(dq, Qp, ic);
+        if (fabsf(dot3(dq, ia[iu])) <= su && fabsf(dot3(dq, ia[iv])) <= sv) em(Qp);
+      }
+    }
+    for (int q = 0; q < 4; q++) {
+      int q2 = (q + 1) & 3;
+      float du = pu[q2] - pu[q], dv = pv[q2] - pv[q];
+      for (int side = 0; side < 4; side++) {
+        float tt;
+        if (side < 2) {
+          float U = side == 0 ? hu : -hu;
+          if (fabsf(du) < 1e-12f) continue;
+          tt = (U - pu[q]) / du;
+          if (!(tt > 0 && tt < 1)) continue;
+          if (fabsf(pv[q] + tt * dv) > hv) continue;
+        } else {
+          float V = side == 2 ? hv : -hv;
+          if (fabsf(dv) < 1e-12f) continue;
+          tt = (V - pv[q]) / dv;
+          if (!(tt > 0 && tt < 1)) continue;
+          if (fabsf(pu[q] + tt * du) > hu) continue;
+        }
+        float X[3];
+        for (int k = 0; k < 3; k++) X[k] = P[q][k] + (P[q2][k] - P[q][k]) * tt;
+        em(X);
+      }
+    }
+    return;
+  }
+  int ea = (bestk - 6) / 3, eb = (bestk - 6) % 3;
+  float pa[3], pb[3];
+  copy3(pa, A.pos);
+  copy3(pb, B.pos);
+  for (int k = 0; k < 3; k++) {
+    if (k != ea) {
+      float s = dot3(a[k], bestn) > 0 ? 1.f : -1.f;
+      for (int q = 0; q < 3; q++) pa[q] += a[k][q] * s * A.size[k];
+    }
+    if (k != eb) {
+      float s = dot3(b[k], bestn) > 0 ? -1.f : 1.f;
+      for (int q = 0; q < 3; q++) pb[q] += b[k][q] * s * B.size[k];
+    }
+  }
+  float s1[3], d1[3], s2[3], d2[3], c1[3], c2[3], pos[3];
+  for (int q = 0; q < 3; q++) {
+    s1[q] = pa[q] - a[ea][q] * A.size[ea]; d1[q] = 2 * a[ea][q] * A.size[ea];
+    s2[q] = pb[q] - b[eb][q] * B.size[eb]; d2[q] = 2 * b[eb][q] * B.size[eb];
+  }
+  seg_seg(s1, d1, s2, d2, c1, c2);
+  for (int q = 0; q < 3; q++) pos[q] = 0.5f * (c1[q] + c2[q]);
+  emit(e, best, pos, bestn);
+}
+
+// ---------------------------------------------------------------------------------------
+// MPR (libccd ccdMPRPenetration), supports inflated by margin/2 (mjccd_support)
+namespace mpr {
+constexpr float EPS = 1.1920928955078125e-07f;  // FLT_EPSILON (libccd CCD_EPS for float)
+__device__ __forceinline__ bool is_zero(float x) { return fabsf(x) < EPS; }
+__device__ __forceinline__ bool eq(float a, float b) {
+  float ab = fabsf(a - b);
+  if (ab < EPS) return true;
+  float fa = fabsf(a), fb = fabsf(b);
+  return fb > fa ? ab < EPS * fb : ab < EPS * fa;
+}
+__device__ __forceinline__ bool veq(const float* a, const float* b) { return eq(a[0], b[0]) && eq(a[1], b[1]) && eq(a[2], b[2]); }
+__device__ __forceinline__ void vnorm(float* v) {
+  float k = 1.0f / sqrtf(dot3(v, v));
+  scl3(v, v, k);
+}
+__device__ __forceinline__ float sgn(float x) { return x < 0 ? -1.f : (x > 0 ? 1.f : 0.f); }
+
+struct Sup { float v[3], v1[3], v2[3]; };
+
+__device__ void gsupport(float* res, const GV& g, const float* dir, float margin) {
+  float ld[3], r[3];
+  mulmtv3(ld, g.mat, dir);
+  const float* s = g.size;
+  if (g.type == GEOM_SPHERE) { scl3(r, ld, s[0]); }
+  else if (g.type == GEOM_CAPSULE) { scl3(r, ld, s[0]); r[2] += sgn(ld[2]) * s[1]; }
+  else if (g.type == GEOM_CYLINDER) {
+    float tmp = sqrtf(ld[0] * ld[0] + ld[1] * ld[1]);
+    if (tmp > MINVAL) { r[0] = ld[0] / tmp * s[0]; r[1] = ld[1] / tmp * s[0]; }
+    else { r[0] = r[1] = 0; }
+    r[2] = sgn(ld[2]) * s[1];
+  } else if (g.type == GEOM_BOX) { for (int k = 0; k < 3; k++) r[k] = sgn(ld[k]) * s[k]; }
+  else { r[0] = r[1] = r[2] = 0; }
+  for (int k = 0; k < 3; k++) r[k] += ld[k] * margin / 2;
+  mulmv3(res, g.mat, r);
+  add3(res, res, g.pos);
+}
+
+struct Ctx { const GV* g1; const GV* g2; float margin, tol; int maxit; };
+
+__device__ __forceinline__ void support(const Ctx& c, const float* dir, Sup& s) {
+  float nd[3];
+  scl3(nd, dir, -1);
+  gsupport(s.v1, *c.g1, dir, c.margin);
+  gsupport(s.v2, *c.g2, nd, c.margin);
+  sub3(s.v, s.v1, s.v2);
+}
+__device__ __forceinline__ void portal_dir(const Sup* p, float* dir) {
+  float a[3], b[3];
+  sub3(a, p[2].v, p[1].v);
+  sub3(b, p[3].v, p[1].v);
+  cross3(dir, a, b);
+  vnorm(dir);
+}
+__device__ __forceinline__ bool reach_tol(const Sup* p, const Sup& v4, const float* dir, float tol) {
+  float dv1 = dot3(p[1].v, dir), dv2 = dot3(p[2].v, dir), dv3 = dot3(p[3].v, dir), dv4 = dot3(v4.v, dir);
+  float d1 = fminf(fminf(dv4 - dv1, dv4 - dv2), dv4 - dv3);
+  return eq(d1, tol) || d1 < tol;
+}
+__device__ __forceinline__ void expand(Sup* p, const Sup& v4) {
+  float v4v0[3];
+  cross3(v4v0, v4.v, p[0].v);
+  float d = dot3(p[1].v, v4v0);
+  if (d > 0) {
+    d = dot3(p[2].v, v4v0);
+    if (d > 0) p[1] = v4; else p[3] = v4;
+  } else {
+    d = dot3(p[3].v, v4v0);
+    if (d > 0) p[2] = v4; else p[1] = v4;
+  }
+}
+__device__ int discover(const Ctx& c, Sup* p) {
+  float dir[3], va[3], vb[3];
+  copy3(p[0].v1, c.g1->pos);
+  copy3(p[0].v2, c.g2->pos);
+  sub3(p[0].v, p[0].v1, p[0].v2);
+  const float zero[3] = {0, 0, 0};
+  if (veq(p[0].v, zero)) p[0].v[0] += EPS * 10;
+  scl3(dir, p[0].v, -1);
+  vnorm(dir);
+  support(c, dir, p[1]);
+  float d = dot3(p[1].v, dir);
+  if (is_zero(d) || d < 0) return -1;
+  cross3(dir, p[0].v, p[1].v);
+  if (is_zero(dot3(dir, dir))) return veq(p[1].v, zero) ? 1 : 2;
+  vnorm(dir);
+  support(c, dir, p[2]);
+  d = dot3(p[2].v, dir);
+  if (is_zero(d) || d < 0) return -1;
+  sub3(va, p[1].v, p[0].v);
+  sub3(vb, p[2].v, p[0].v);
+  cross3(dir, va, vb);
+  vnorm(dir);
+  if (dot3(dir, p[0].v) > 0) {
+    Sup t = p[1]; p[1] = p[2]; p[2] = t;
+    scl3(dir, dir, -1);
+  }
+  for (int it = 0; it < 1000; it++) {
+    support(c, dir, p[3]);
+    d = dot3(p[3].v, dir);
+    if (is_zero(d) || d < 0) return -1;
+    bool cont = false;
+    cross3(va, p[1].v, p[3].v);
+    d = dot3(va, p[0].v);
+    if (d < 0 && !is_zero(d)) { p[2] = p[3]; cont = true; }
+    if (!cont) {
+      cross3(va, p[3].v, p[2].v);
+      d = dot3(va, p[0].v);
+      if (d < 0 && !is_zero(d)) { p[1] = p[3]; cont = true; }
+    }
+    if (!cont) return 0;
+    sub3(va, p[1].v, p[0].v);
+    sub3(vb, p[2].v, p[0].v);
+    cross3(dir, va, vb);
+    vnorm(dir);
+  }
+  return -1;
+}
+__device__ int refine(const Ctx& c, Sup* p) {
+  float dir[3];
+  Sup v4;
+  for (int it = 0; it <= c.maxit; it++) {
+    portal_dir(p, dir);
+    float d = dot3(dir, p[1].v);
+    if (is_zero(d) || d > 0) return 0;
+    support(c, dir, v4);
+    float d4 = dot3(v4.v, dir);
+    if (!(is_zero(d4) || d4 > 0) || reach_tol(p, v4, dir, c.tol)) return -1;
+    expand(p, v4);
+  }
+  return -1;
+}
+__device__ float pseg2(const float* P, const float* x0, const float* b, float* w) {
+  float dd[3], a[3];
+  sub3(dd, b, x0);
+  sub3(a, x0, P);
+  float t = -dot3(a, dd) / dot3(dd, dd);
+  if (t < 0 || is_zero(t)) copy3(w, x0);
+  else if (t > 1 || eq(t, 1)) copy3(w, b);
+  else for (int k = 0; k < 3; k++) w[k] = x0[k] + dd[k] * t;
+  float df[3];
+  sub3(df, w, P);
+  return dot3(df, df);
+}
+__device__ float ptri2(const float* P, const float* x0, const float* B, const float* C, float* w) {
+  float d1[3], d2[3], a[3];
+  sub3(d1, B, x0);
+  sub3(d2, C, x0);
+  sub3(a, x0, P);
+  float v = dot3(d1, d1), ww = dot3(d2, d2), p = dot3(a, d1), q = dot3(a, d2), r = dot3(d1, d2);
+  float dd = ww * v - r * r, s, t;
+  if (is_zero(dd)) { s = t = -1; }
+  else { s = (q * r - ww * p) / dd; t = (-s * r - q) / ww; }
+  if ((is_zero(s) || s > 0) && (eq(s, 1) || s < 1) && (is_zero(t) || t > 0) && (eq(t, 1) || t < 1) &&
+      (eq(t + s, 1) || t + s < 1)) {
+    for (int k = 0; k < 3; k++) w[k] = x0[k] + d1[k] * s + d2[k] * t;
+    float df[3];
+    sub3(df, w, P);
+    return dot3(df, df);
+  }
+  float w2[3];
+  float dist = pseg2(P, x0, B, w);
+  float d2s = pseg2(P, x0, C, w2);
+  if (d2s < dist) { dist = d2s; copy3(w, w2); }
+  d2s = pseg2(P, B, C, w2);
+  if (d2s < dist) { dist = d2s; copy3(w, w2); }
+  return dist;
+}
+__device__ void find_pos(const Sup* p, float* pos) {
+  float dir[3], vec[3], b[4];
+  portal_dir(p, dir);
+  cross3(vec, p[1].v, p[2].v); b[0] = dot3(vec, p[3].v);
+  cross3(vec, p[3].v, p[2].v); b[1] = dot3(vec, p[0].v);
+  cross3(vec, p[0].v, p[1].v); b[2] = dot3(vec, p[3].v);
+  cross3(vec, p[2].v, p[1].v); b[3] = dot3(vec, p[0].v);
+  float sum = b[0] + b[1] + b[2] + b[3];
+  if (is_zero(sum) || sum < 0) {
+    b[0] = 0;
+    cross3(vec, p[2].v, p[3].v); b[1] = dot3(vec, dir);
+    cross3(vec, p[3].v, p[1].v); b[2] = dot3(vec, dir);
+    cross3(vec, p[1].v, p[2].v); b[3] = dot3(vec, dir);
+    sum = b[1] + b[2] + b[3];
+  }
+  float inv = 1.0f / sum, p1[3] = {0, 0, 0}, p2[3] = {0, 0, 0};
+  for (int i = 0; i < 4; i++)
+    for (int k = 0; k < 3; k++) { p1[k] += p[i].v1[k] * b[i]; p2[k] += p[i].v2[k] * b[i]; }
+  for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p1[k] + p2[k]) * inv;
+}
+__device__ int penetration(const Ctx& c, float* depth, float* dir, float* pos) {
+  Sup p[4];
+  int res = discover(c, p);
+  if (res < 0) return -1;
+  if (res == 1) {
+    *depth = 0;
+    dir[0] = dir[1] = dir[2] = 0;
+    for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p[1].v1[k] + p[1].v2[k]);
+    return 0;
+  }
+  if (res == 2) {
+    for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p[1].v1[k] + p[1].v2[k]);
+    copy3(dir, p[1].v);
+    *depth = sqrtf(dot3(dir, dir));
+    vnorm(dir);
+    return 0;
+  }
+  if (refine(c, p) < 0) return -1;
+  Sup v4;
+  float pd[3];
+  for (int it = 0;; it++) {
+    portal_dir(p, pd);
+    support(c, pd, v4);
+    if (reach_tol(p, v4, pd, c.tol) || it > c.maxit) {
+      const float zero[3] = {0, 0, 0};
+      *depth = sqrtf(ptri2(zero, p[1].v, p[2].v, p[3].v, dir));
+      if (is_zero(*depth)) dir[0] = dir[1] = dir[2] = 0;
+      else vnorm(dir);
+      find_pos(p, pos);
+      return 0;
+    }
+    expand(p, v4);
+  }
+}
+}  // namespace mpr
+
+__device__ void c_convex(const DModel& m, const GV& a, const GV& b, float margin, Emit& e) {
+  mpr::Ctx ctx{&a, &b, margin, m.mpr_tolerance, m.mpr_iterations};
+  float depth, dir[3], pos[3];
+  if (mpr::penetration(ctx, &depth, dir, pos) != 0) return;
+  if (dir[0] == 0 && dir[1] == 0 && dir[2] == 0) return;
+  float dist = margin - depth;
+  if (dist > margin) return;
+  emit(e, dist, pos, dir);
+}
+
+// ---------------------------------------------------------------------------------------
+__device__ void collide_pair(const DModel& m, Env& s, int pair) {
+  int g1 = m.cp_g1[pair], g2 = m.cp_g2[pair];
+  GV a, b;
+  a.type = m.geom_type[g1];
+  b.type = m.geom_type[g2];
+  for (int k = 0; k < 3; k++) {
+    a.pos[k] = s.gxpos[g1][k]; b.pos[k] = s.gxpos[g2][k];
+    a.size[k] = s.gsize[g1][k]; b.size[k] = s.gsize[g2][k];
+  }
+  float margin = m.cp_margin[pair];
+  if (a.type != GEOM_PLANE && b.type != GEOM_PLANE) {
+    float dif[3];
+    sub3(dif, a.pos, b.pos);
+    if (norm3(dif) > m.geom_rbound[g1] + m.geom_rbound[g2] + margin) return;
+  }
+  for (int k = 0; k < 9; k++) { a.mat[k] = s.gxmat[g1][k]; b.mat[k] = s.gxmat[g2][k]; }
+  Emit e{&s, pair, 0};
+  switch (a.type) {
+    case GEOM_PLANE:
+      if (b.type == GEOM_SPHERE) c_plane_sphere(a.pos, a.mat, b.pos, b.size[0], margin, e);
+      else if (b.type == GEOM_CAPSULE) c_plane_capsule(a, b, margin, e);
+      else if (b.type == GEOM_CYLINDER) c_plane_cylinder(a, b, margin, e);
+      else if (b.type == GEOM_BOX) c_plane_box(a, b, margin, e);
+      break;
+    case GEOM_SPHERE:
+      if (b.type == GEOM_SPHERE) c_sphere_sphere(a.pos, a.size[0], b.pos, b.size[0], margin, e);
+      else if (b.type == GEOM_CAPSULE) c_sphere_capsule(a, b, margin, e);
+      else if (b.type == GEOM_CYLINDER) c_convex(m, a, b, margin, e);
+      else if (b.type == GEOM_BOX) c_sphere_box_pt(a.pos, a.size[0], b, margin, e);
+      break;
+    case GEOM_CAPSULE:
+      if (b.type == GEOM_CAPSULE) c_capsule_capsule(a, b, margin, e);
+      else if (b.type == GEOM_CYLINDER) c_convex(m, a, b, margin, e);
+      else if (b.type == GEOM_BOX) c_capsule_box(a, b, margin, e);
+      break;
+    case GEOM_CYLINDER:
+      c_convex(m, a, b, margin, e);
+      break;
+    case GEOM_BOX:
+      if (b.type == GEOM_BOX) c_box_box(a, b, margin, e);
+      break;
+  }
+}
+
+}  // namespace aw

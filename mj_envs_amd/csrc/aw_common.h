@@ -1,0 +1,285 @@
+// aw_common.h -- device model, per-env LDS layout and wave primitives for the Adroit kernels.
+//
+// Execution model (MI355X / gfx950): one 64-lane wavefront simulates one env; a workgroup is
+// exactly one wave, so the per-env working set lives in that workgroup's LDS and lanes map to
+// bodies / dofs / geom pairs / constraint rows as each stage needs.  Matrices whose rows are
+// consumed lane-parallel (M, H, M + hD) live in VGPRs, one row per lane, and are factored with
+// v_readlane broadcasts (no LDS round trips in the Cholesky inner loop).  The model (fp32,
+// ~25 KB) is read from HBM through the L1/L2; every wave reads the same bytes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace aw {
+
+constexpr int MAXV = 36;      // dofs (relocate: 36)
+constexpr int VS = 37;        // odd row stride for [.][MAXV] LDS matrices (bank-conflict free)
+constexpr int MAXB = 32;      // bodies incl. world
+constexpr int MAXG = 36;      // collidable geoms (compact list)
+constexpr int MAXS = 32;      // sites
+constexpr int MAXT = 44;      // tendons
+constexpr int MAXU = 30;      // actuators
+constexpr int MAXCON = 32;    // contacts kept per env (oracle uses the same cap)
+constexpr int MAXEFC = 128;   // constraint rows
+constexpr int MAXDENSE = 64;  // dense (contact) constraint rows; also the noslip edge cap
+constexpr int MAXP = 8;       // per-env model parameters
+constexpr int MAXLEV = 16;    // kinematic tree depth
+constexpr int MAXTOUCH = 4;   // task touch sensors
+constexpr int MAXPAIRCON = 8; // contacts per geom pair
+
+constexpr float MINVAL = 1e-15f;
+
+enum { GEOM_PLANE = 0, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_CYLINDER = 5, GEOM_BOX = 6 };
+enum { JNT_SLIDE = 2, JNT_HINGE = 3 };
+enum { C_FRIC_DOF = 0, C_FRIC_TEN = 1, C_LIM_JNT = 2, C_LIM_TEN = 3, C_CON_FRICTIONLESS = 4, C_CON_PYRAMIDAL = 5 };
+enum { S_SAT = 0, S_QUAD = 1, S_LNEG = 2, S_LPOS = 3 };
+
+// disable bits (MuJoCo 2.1 mjtDisableBit values + ours), see include/adroit_wave.h
+enum {
+  DSBL_CONSTRAINT = 1 << 0, DSBL_FRICTIONLOSS = 1 << 2, DSBL_LIMIT = 1 << 3, DSBL_CONTACT = 1 << 4,
+  DSBL_PASSIVE = 1 << 5, DSBL_GRAVITY = 1 << 6, DSBL_CLAMPCTRL = 1 << 7, DSBL_WARMSTART = 1 << 8,
+  DSBL_ACTUATION = 1 << 10, DSBL_REFSAFE = 1 << 11, DSBL_SENSOR = 1 << 12, DSBL_NOSLIP = 1 << 14,
+  DSBL_EULERDAMP = 1 << 15,
+};
+enum { ST_BADQPOS = 1, ST_BADQVEL = 2, ST_BADQACC = 4, ST_CON_OVERFLOW = 8, ST_EFC_OVERFLOW = 16 };
+
+// ---------------------------------------------------------------------------------------
+// Device model: flat fp32/int32 arrays in one HBM allocation (built on the host from the blob).
+struct DModel {
+  int nq, nv, nu, nbody, njnt, ngeom, nsite, ntendon, npairall, nlevel;
+  int nfl;                // dofs with frictionloss (rows 0..nfl-1 are these, in dof order)
+  int ntouch;
+  int ndraw;              // reset uniform draws
+  int task_kind, frame_skip, horizon, obs_dim, nparam, variation;
+  int iterations, noslip_iterations, mpr_iterations, disableflags;
+  float timestep, gravity[3], tolerance, noslip_tolerance, mpr_tolerance, meaninertia;
+  float pen_length, tar_length;
+
+  const int* body_parentid; const int* body_rootid; const int* body_dofnum; const int* body_dofadr;
+  const int* body_subtree_end; const int* level_start; const int* level_body;
+  const float* body_pos; const float* body_quat; const float* body_ipos; const float* body_iquat;
+  const float* body_mass; const float* body_inertia; const float* body_invweight0;
+  const float* body_subtreemass;
+  const unsigned long long* body_dofmask;  // dofs moving the body (ancestor chain)
+
+  const int* jnt_type; const int* jnt_bodyid; const int* jnt_limited;
+  const float* jnt_pos; const float* jnt_axis; const float* jnt_range; const float* jnt_margin;
+  const float* jnt_solref; const float* jnt_solimp;
+
+  const int* dof_bodyid; const int* dof_act;  // actuator driving the dof or -1
+  const int* fl_dof; const int* fl_row;       // frictionloss row r -> dof, dof -> row (or -1)
+  const unsigned long long* dof_ancmask;      // strict ancestor dofs
+  const float* dof_armature; const float* dof_damping; const float* dof_frictionloss;
+  const float* dof_invweight0; const float* dof_solref; const float* dof_solimp;
+
+  const int* geom_type; const int* geom_bodyid;
+  const float* geom_pos; const float* geom_quat; const float* geom_size; const float* geom_rbound;
+
+  const int* site_bodyid; const float* site_pos; const float* site_quat;
+  const int* touch_site; const int* touch_adr; const int* touch_type; const float* touch_size;
+
+  const int* ten_d0; const int* ten_d1; const int* ten_limited;
+  const float* ten_c0; const float* ten_c1; const float* ten_range; const float* ten_margin;
+  const float* ten_solref; const float* ten_solimp; const float* ten_invweight0;
+
+  const int* act_ctrllimited; const int* act_forcelimited;
+  const float* act_gear; const float* act_gain; const float* act_bias; const float* act_ctrlrange;
+  const float* act_forcerange;
+
+  // explicit pairs first, then dynamic candidates; params pre-mixed on the host
+  const int* cp_g1; const int* cp_g2; const int* cp_condim;
+  const float* cp_friction; const float* cp_solref; const float* cp_solimp; const float* cp_margin;
+  const float* cp_gap;
+
+  const int* task_idx; const int* param_field; const int* param_obj; const int* param_comp;
+  const float* act_mid; const float* act_rng; const float* param_default;
+  const float* draw_lo; const float* draw_hi;
+};
+
+// ---------------------------------------------------------------------------------------
+// Per-env working set in LDS (one wave per workgroup, one env per wave).
+struct __attribute__((aligned(16))) Env {
+  // state and lane-per-dof vectors
+  float qpos[MAXV], qvel[MAXV], warm[MAXV], ctrl[MAXV];
+  float qacc[MAXV], qacc_smooth[MAXV], qfrc_smooth[MAXV], qfrc_con[MAXV], vec[MAXV], vec2[MAXV];
+  // per-env copies of the overridable model fields
+  float bpos[MAXB][3], bquat[MAXB][4], bmass[MAXB];
+  float spos[MAXS][3];
+  float gpos[MAXG][3], gsize[MAXG][3];
+  // position stage
+  float xpos[MAXB][3], xquat[MAXB][4], xmat[MAXB][9], xipos[MAXB][3], subcom[MAXB][3];
+  float cinert[MAXB][10];
+  union {
+    struct { float crb[MAXB][10]; float buf[MAXV][6]; } p;     // M build
+    struct { float cvel[MAXB][6]; float cacc[MAXB][6]; } v;    // velocity stage (cacc -> cfrc)
+  } u1;
+  union {
+    struct { float xaxis[MAXV][3]; float xanchor[MAXV][3]; } j;
+    float cdof_dot[MAXV][6];
+  } u2;
+  float cdof[MAXV][6];
+  float gxpos[MAXG][3], gxmat[MAXG][9];
+  float sxpos[MAXS][3];
+  float txmat[MAXTOUCH][9];
+  float tlen[MAXT];
+  float L[MAXV][VS];      // Cholesky rows (M, then H, then M + hD); also sparse-H staging
+  // contacts
+  int ncon;
+  int con_key[MAXCON], con_pair[MAXCON], con_efc[MAXCON];
+  float con_dist[MAXCON], con_pos[MAXCON][3], con_frame[MAXCON][9];
+  // constraint rows: [0, nsparse) sparse (<= 2 nonzeros), [nsparse, nefc) dense (J rows)
+  int nefc, nsparse, ndense, npyr0;   // npyr0: first pyramidal dense row
+  unsigned char efc_type[MAXEFC];
+  signed char efc_i0[MAXEFC], efc_i1[MAXEFC];
+  short efc_id[MAXEFC];
+  float efc_v0[MAXEFC], efc_v1[MAXEFC], efc_pm[MAXEFC], efc_floss[MAXEFC], efc_D[MAXEFC];
+  float efc_aref[MAXEFC], efc_dA[MAXEFC], efc_force[MAXEFC];
+  float J[MAXDENSE][VS];
+  float rowbuf[MAXEFC];
+  float ns_a[MAXDENSE][3];   // noslip: per pyramid edge pair A11, A22, A12 (stored at first edge)
+  float touch[MAXTOUCH];
+  unsigned status;
+  int red_i;
+  float red_f[4];
+};
+
+// ---------------------------------------------------------------------------------------
+// wave primitives
+__device__ __forceinline__ float rlane(float x, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
+}
+__device__ __forceinline__ int rlane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ void wsync() { __syncthreads(); }
+
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+__device__ __forceinline__ float wave_max(float x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
+  return x;
+}
+// exclusive prefix sum of small non-negative ints across the wave
+__device__ __forceinline__ int wave_excl_scan(int x, int lane, int* total) {
+  int v = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int y = __shfl_up(v, o, 64);
+    if (lane >= o) v += y;
+  }
+  *total = __shfl(v, 63, 64);
+  return v - x;
+}
+
+// ---------------------------------------------------------------------------------------
+// fp32 3D helpers
+__device__ __forceinline__ float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+__device__ __forceinline__ void cross3(float* r, const float* a, const float* b) {
+  float t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+__device__ __forceinline__ void sub3(float* r, const float* a, const float* b) { r[0] = a[0] - b[0]; r[1] = a[1] - b[1]; r[2] = a[2] - b[2]; }
+__device__ __forceinline__ void add3(float* r, const float* a, const float* b) { r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2]; }
+__device__ __forceinline__ void scl3(float* r, const float* a, float s) { r[0] = a[0] * s; r[1] = a[1] * s; r[2] = a[2] * s; }
+__device__ __forceinline__ void copy3(float* r, const float* a) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; }
+__device__ __forceinline__ float norm3(const float* a) { return sqrtf(dot3(a, a)); }
+__device__ __forceinline__ float normalize3(float* a) {
+  float n = norm3(a);
+  if (n < MINVAL) { a[0] = 1; a[1] = 0; a[2] = 0; return n; }
+  float in = 1.0f / n;
+  a[0] *= in; a[1] *= in; a[2] *= in;
+  return n;
+}
+__device__ __forceinline__ void mulmv3(float* r, const float* m, const float* v) {
+  float t0 = m[0] * v[0] + m[1] * v[1] + m[2] * v[2];
+  float t1 = m[3] * v[0] + m[4] * v[1] + m[5] * v[2];
+  float t2 = m[6] * v[0] + m[7] * v[1] + m[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+__device__ __forceinline__ void mulmtv3(float* r, const float* m, const float* v) {
+  float t0 = m[0] * v[0] + m[3] * v[1] + m[6] * v[2];
+  float t1 = m[1] * v[0] + m[4] * v[1] + m[7] * v[2];
+  float t2 = m[2] * v[0] + m[5] * v[1] + m[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+__device__ __forceinline__ void mulq(float* r, const float* a, const float* b) {
+  float t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  float t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  float t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  float t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
+}
+__device__ __forceinline__ void rotvq(float* r, const float* v, const float* q) {
+  float u[3] = {q[1], q[2], q[3]}, t[3], t2[3];
+  cross3(t, u, v);
+  scl3(t, t, 2.0f);
+  cross3(t2, u, t);
+  r[0] = v[0] + q[0] * t[0] + t2[0];
+  r[1] = v[1] + q[0] * t[1] + t2[1];
+  r[2] = v[2] + q[0] * t[2] + t2[2];
+}
+__device__ __forceinline__ void q2m(float* m, const float* q) {
+  float w = q[0], x = q[1], y = q[2], z = q[3];
+  m[0] = 1 - 2 * (y * y + z * z); m[1] = 2 * (x * y - w * z); m[2] = 2 * (x * z + w * y);
+  m[3] = 2 * (x * y + w * z); m[4] = 1 - 2 * (x * x + z * z); m[5] = 2 * (y * z - w * x);
+  m[6] = 2 * (x * z - w * y); m[7] = 2 * (y * z + w * x); m[8] = 1 - 2 * (x * x + y * y);
+}
+__device__ __forceinline__ void normq(float* q) {
+  float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < MINVAL) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  float in = 1.0f / n;
+  q[0] *= in; q[1] *= in; q[2] *= in; q[3] *= in;
+}
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+// mju_makeFrame
+__device__ __forceinline__ void make_frame(float* f) {
+  normalize3(f);
+  if (norm3(f + 3) < 0.5f) {
+    if (fabsf(f[1]) < 0.5f) { f[3] = 0; f[4] = 1; f[5] = 0; }
+    else { f[3] = 0; f[4] = 0; f[5] = 1; }
+  }
+  float d = dot3(f, f + 3);
+  f[3] -= d * f[0]; f[4] -= d * f[1]; f[5] -= d * f[2];
+  normalize3(f + 3);
+  cross3(f + 6, f, f + 3);
+}
+
+// spatial algebra, MuJoCo layout (motion = [ang; lin]; cinert = [Ixx Iyy Izz Ixy Ixz Iyz mc m])
+__device__ __forceinline__ void mul_inert_vec(float* r, const float* i, const float* v) {
+  r[0] = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
+  r[1] = i[3] * v[0] + i[1] * v[1] + i[5] * v[2] + i[8] * v[3] - i[6] * v[5];
+  r[2] = i[4] * v[0] + i[5] * v[1] + i[2] * v[2] - i[7] * v[3] + i[6] * v[4];
+  r[3] = i[8] * v[1] - i[7] * v[2] + i[9] * v[3];
+  r[4] = i[6] * v[2] - i[8] * v[0] + i[9] * v[4];
+  r[5] = i[7] * v[0] - i[6] * v[1] + i[9] * v[5];
+}
+__device__ __forceinline__ void cross_motion(float* r, const float* v, const float* u) {
+  float t[6];
+  t[0] = -v[2] * u[1] + v[1] * u[2];
+  t[1] = v[2] * u[0] - v[0] * u[2];
+  t[2] = -v[1] * u[0] + v[0] * u[1];
+  t[3] = -v[2] * u[4] + v[1] * u[5] - v[5] * u[1] + v[4] * u[2];
+  t[4] = v[2] * u[3] - v[0] * u[5] + v[5] * u[0] - v[3] * u[2];
+  t[5] = -v[1] * u[3] + v[0] * u[4] - v[4] * u[0] + v[3] * u[1];
+#pragma unroll
+  for (int k = 0; k < 6; k++) r[k] = t[k];
+}
+__device__ __forceinline__ void cross_force(float* r, const float* v, const float* f) {
+  float t[6];
+  t[0] = -v[2] * f[1] + v[1] * f[2] - v[5] * f[4] + v[4] * f[5];
+  t[1] = v[2] * f[0] - v[0] * f[2] + v[5] * f[3] - v[3] * f[5];
+  t[2] = -v[1] * f[0] + v[0] * f[1] - v[4] * f[3] + v[3] * f[4];
+  t[3] = -v[2] * f[4] + v[1] * f[5];
+  t[4] = v[2] * f[3] - v[0] * f[5];
+  t[5] = -v[1] * f[3] + v[0] * f[4];
+#pragma unroll
+  for (int k = 0; k < 6; k++) r[k] = t[k];
+}
+__device__ __forceinline__ float dot6(const float* a, const float* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+
+}  // namespace aw

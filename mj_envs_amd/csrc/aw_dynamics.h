@@ -1,0 +1,284 @@
+// aw_dynamics.h -- position/velocity stages of mj_step for one env per wave (fp32).
+//
+// Lane maps: bodies (kinematics in tree-level order, subtree sums over DFS ranges), dofs
+// (cdof, M rows, RNE projections), geoms / sites.  Restates MuJoCo 2.1 mj_kinematics,
+// mj_comPos, mj_tendon (fixed), mj_crb, mj_comVel, mj_rne (flg_acc = 0), mj_passive,
+// mj_fwdActuation (see oracle/mjstep.cc for the fp64 statement of the same stages).
+#pragma once
+#include "aw_common.h"
+
+namespace aw {
+
+// ---------------------------------------------------------------------------------------
+// stage the per-env model copies (body_pos/quat/mass, site_pos, geom_pos/size) + overrides
+__device__ void stage_model(const DModel& m, Env& s, const float* params, int lane) {
+  for (int b = lane; b < m.nbody; b += 64) {
+    for (int k = 0; k < 3; k++) s.bpos[b][k] = m.body_pos[3 * b + k];
+    for (int k = 0; k < 4; k++) s.bquat[b][k] = m.body_quat[4 * b + k];
+    s.bmass[b] = m.body_mass[b];
+  }
+  for (int i = lane; i < m.nsite; i += 64)
+    for (int k = 0; k < 3; k++) s.spos[i][k] = m.site_pos[3 * i + k];
+  for (int g = lane; g < m.ngeom; g += 64)
+    for (int k = 0; k < 3; k++) { s.gpos[g][k] = m.geom_pos[3 * g + k]; s.gsize[g][k] = m.geom_size[3 * g + k]; }
+  wsync();
+  if (lane == 0) {
+    for (int p = 0; p < m.nparam; p++) {
+      float v = params ? params[p] : m.param_default[p];
+      int o = m.param_obj[p], c = m.param_comp[p];
+      switch (m.param_field[p]) {
+        case 0: s.bpos[o][c] = v; break;
+        case 1: s.bquat[o][c] = v; break;
+        case 2: s.spos[o][c] = v; break;
+        case 3: s.bmass[o] = v; break;
+        case 4: s.gpos[o][c] = v; break;
+        case 5: s.gsize[o][c] = v; break;
+      }
+    }
+  }
+  wsync();
+}
+
+// mj_kinematics (+ local2global for geoms, sites)
+__device__ void stage_kinematics(const DModel& m, Env& s, int lane) {
+  if (lane == 0) {
+    s.xpos[0][0] = s.xpos[0][1] = s.xpos[0][2] = 0;
+    s.xquat[0][0] = 1; s.xquat[0][1] = s.xquat[0][2] = s.xquat[0][3] = 0;
+    for (int k = 0; k < 9; k++) s.xmat[0][k] = (k % 4 == 0) ? 1.f : 0.f;
+  }
+  wsync();
+  for (int lev = 1; lev < m.nlevel; lev++) {
+    int beg = m.level_start[lev], end = m.level_start[lev + 1];
+    for (int idx = beg + lane; idx < end; idx += 64) {
+      int b = m.level_body[idx], p = m.body_parentid[b];
+      float xp[3], xq[4];
+      mulmv3(xp, s.xmat[p], s.bpos[b]);
+      add3(xp, xp, s.xpos[p]);
+      mulq(xq, s.xquat[p], s.bquat[b]);
+      int da = m.body_dofadr[b];
+      for (int k = 0; k < m.body_dofnum[b]; k++) {
+        int j = da + k;
+        float axis[3], xaxis[3], xanchor[3], jp[3];
+        for (int q = 0; q < 3; q++) { axis[q] = m.jnt_axis[3 * j + q]; jp[q] = m.jnt_pos[3 * j + q]; }
+        rotvq(xaxis, axis, xq);
+        rotvq(xanchor, jp, xq);
+        add3(xanchor, xanchor, xp);
+        float q = s.qpos[j];
+        if (m.jnt_type[j] == JNT_SLIDE) {
+          for (int c = 0; c < 3; c++) xp[c] += xaxis[c] * q;
+        } else {
+          float sn, cs, ql[4], v[3];
+          sn = sinf(0.5f * q);
+          cs = cosf(0.5f * q);
+          ql[0] = cs; ql[1] = axis[0] * sn; ql[2] = axis[1] * sn; ql[3] = axis[2] * sn;
+          mulq(xq, xq, ql);
+          rotvq(v, jp, xq);
+          sub3(xp, xanchor, v);
+        }
+        copy3(s.u2.j.xaxis[j], xaxis);
+        copy3(s.u2.j.xanchor[j], xanchor);
+      }
+      normq(xq);
+      copy3(s.xpos[b], xp);
+      for (int c = 0; c < 4; c++) s.xquat[b][c] = xq[c];
+      q2m(s.xmat[b], xq);
+    }
+    wsync();
+  }
+  // geoms (compact collidable list), sites, inertial frames
+  for (int g = lane; g < m.ngeom; g += 64) {
+    int b = m.geom_bodyid[g];
+    float v[3], q[4], gq[4];
+    mulmv3(v, s.xmat[b], s.gpos[g]);
+    add3(s.gxpos[g], v, s.xpos[b]);
+    for (int c = 0; c < 4; c++) gq[c] = m.geom_quat[4 * g + c];
+    mulq(q, s.xquat[b], gq);
+    q2m(s.gxmat[g], q);
+  }
+  for (int i = lane; i < m.nsite; i += 64) {
+    int b = m.site_bodyid[i];
+    float v[3];
+    mulmv3(v, s.xmat[b], s.spos[i]);
+    add3(s.sxpos[i], v, s.xpos[b]);
+  }
+  if (lane < m.ntouch) {
+    int i = m.touch_site[lane], b = m.site_bodyid[i];
+    float q[4], sq[4];
+    for (int c = 0; c < 4; c++) sq[c] = m.site_quat[4 * i + c];
+    mulq(q, s.xquat[b], sq);
+    q2m(s.txmat[lane], q);
+  }
+  for (int b = lane; b < m.nbody; b += 64) {
+    float v[3], ip[3];
+    for (int c = 0; c < 3; c++) ip[c] = m.body_ipos[3 * b + c];
+    mulmv3(v, s.xmat[b], ip);
+    add3(s.xipos[b], v, s.xpos[b]);
+  }
+  wsync();
+}
+
+// mj_comPos: subtree com (divided by the compile-time subtree mass), cinert, cdof
+__device__ void stage_com(const DModel& m, Env& s, int lane) {
+  for (int b = lane; b < m.nbody; b += 64) {
+    float acc[3] = {0, 0, 0};
+    for (int d = b; d < m.body_subtree_end[b]; d++) {
+      float md = s.bmass[d];
+      acc[0] += md * s.xipos[d][0]; acc[1] += md * s.xipos[d][1]; acc[2] += md * s.xipos[d][2];
+    }
+    float stm = m.body_subtreemass[b];
+    if (stm < MINVAL) copy3(s.subcom[b], s.xipos[b]);
+    else scl3(s.subcom[b], acc, 1.0f / stm);
+  }
+  wsync();
+  for (int b = lane; b < m.nbody; b += 64) {
+    float* c = s.cinert[b];
+    if (b == 0) { for (int k = 0; k < 10; k++) c[k] = 0; continue; }
+    float q[4], iq[4], R[9], dif[3];
+    for (int k = 0; k < 4; k++) iq[k] = m.body_iquat[4 * b + k];
+    mulq(q, s.xquat[b], iq);
+    q2m(R, q);
+    const float* I = &m.body_inertia[3 * b];
+    float mass = s.bmass[b];
+    sub3(dif, s.xipos[b], s.subcom[m.body_rootid[b]]);
+    float T[9];
+    for (int a = 0; a < 3; a++)
+      for (int bb = 0; bb < 3; bb++)
+        T[3 * a + bb] = R[3 * a] * I[0] * R[3 * bb] + R[3 * a + 1] * I[1] * R[3 * bb + 1] + R[3 * a + 2] * I[2] * R[3 * bb + 2];
+    c[0] = T[0] + mass * (dif[1] * dif[1] + dif[2] * dif[2]);
+    c[1] = T[4] + mass * (dif[0] * dif[0] + dif[2] * dif[2]);
+    c[2] = T[8] + mass * (dif[0] * dif[0] + dif[1] * dif[1]);
+    c[3] = T[1] - mass * dif[0] * dif[1];
+    c[4] = T[2] - mass * dif[0] * dif[2];
+    c[5] = T[5] - mass * dif[1] * dif[2];
+    c[6] = mass * dif[0]; c[7] = mass * dif[1]; c[8] = mass * dif[2];
+    c[9] = mass;
+  }
+  if (lane < m.nv) {
+    int j = lane, b = m.dof_bodyid[j];
+    float* cd = s.cdof[j];
+    const float* axis = s.u2.j.xaxis[j];
+    if (m.jnt_type[j] == JNT_SLIDE) {
+      cd[0] = cd[1] = cd[2] = 0;
+      copy3(cd + 3, axis);
+    } else {
+      float off[3];
+      sub3(off, s.subcom[m.body_rootid[b]], s.u2.j.xanchor[j]);
+      copy3(cd, axis);
+      cross3(cd + 3, axis, off);
+    }
+  }
+  for (int t = lane; t < m.ntendon; t += 64) {
+    int d1 = m.ten_d1[t];
+    s.tlen[t] = m.ten_c0[t] * s.qpos[m.ten_d0[t]] + (d1 >= 0 ? m.ten_c1[t] * s.qpos[d1] : 0.f);
+  }
+  wsync();
+}
+
+// mj_crb -> M row per lane (registers).  M[i][k] = cdof_k . (crb_{body i} cdof_i) for k an
+// ancestor of i, symmetric for descendants, + armature on the diagonal.
+template <int NV>
+__device__ void stage_crb(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
+  for (int b = lane; b < m.nbody; b += 64) {
+    float acc[10];
+    for (int k = 0; k < 10; k++) acc[k] = 0;
+    if (b > 0)
+      for (int d = b; d < m.body_subtree_end[b]; d++)
+        for (int k = 0; k < 10; k++) acc[k] += s.cinert[d][k];
+    for (int k = 0; k < 10; k++) s.u1.p.crb[b][k] = acc[k];
+  }
+  wsync();
+  const int li = lane < NV ? lane : NV - 1;
+  float ci[6], bi[6];
+  for (int k = 0; k < 6; k++) ci[k] = s.cdof[li][k];
+  mul_inert_vec(bi, s.u1.p.crb[m.dof_bodyid[li]], ci);
+  for (int k = 0; k < 6; k++) s.u1.p.buf[li][k] = bi[k];
+  wsync();
+  const unsigned long long anc = m.dof_ancmask[li];
+  const float arm = m.dof_armature[li];
+#pragma unroll
+  for (int k = 0; k < NV; k++) {
+    float ck[6], bk[6];
+    for (int c = 0; c < 6; c++) { ck[c] = s.cdof[k][c]; bk[c] = s.u1.p.buf[k][c]; }
+    const unsigned long long anck = m.dof_ancmask[k];
+    float v;
+    if (k == li) v = dot6(ci, bi) + arm;
+    else if ((anc >> k) & 1ull) v = dot6(ck, bi);
+    else if ((anck >> li) & 1ull) v = dot6(ci, bk);
+    else v = 0.f;
+    Mrow[k] = v;
+  }
+  wsync();
+}
+
+// mj_comVel + mj_rne(flg_acc=0) + mj_passive + mj_fwdActuation -> qfrc_smooth
+__device__ void stage_velocity(const DModel& m, Env& s, int lane) {
+  float (*cvel)[6] = s.u1.v.cvel;
+  float (*cacc)[6] = s.u1.v.cacc;
+  if (lane == 0) {
+    for (int k = 0; k < 6; k++) { cvel[0][k] = 0; cacc[0][k] = 0; }
+    if (!(m.disableflags & DSBL_GRAVITY)) { cacc[0][3] = -m.gravity[0]; cacc[0][4] = -m.gravity[1]; cacc[0][5] = -m.gravity[2]; }
+  }
+  wsync();
+  for (int lev = 1; lev < m.nlevel; lev++) {
+    int beg = m.level_start[lev], end = m.level_start[lev + 1];
+    for (int idx = beg + lane; idx < end; idx += 64) {
+      int b = m.level_body[idx], p = m.body_parentid[b];
+      float cv[6], ca[6];
+      for (int k = 0; k < 6; k++) { cv[k] = cvel[p][k]; ca[k] = cacc[p][k]; }
+      int da = m.body_dofadr[b];
+      for (int q = 0; q < m.body_dofnum[b]; q++) {
+        int j = da + q;
+        float cd[6], cdd[6], qv = s.qvel[j];
+        for (int k = 0; k < 6; k++) cd[k] = s.cdof[j][k];
+        cross_motion(cdd, cv, cd);
+        for (int k = 0; k < 6; k++) { s.u2.cdof_dot[j][k] = cdd[k]; cv[k] += cd[k] * qv; ca[k] += cdd[k] * qv; }
+      }
+      for (int k = 0; k < 6; k++) { cvel[b][k] = cv[k]; cacc[b][k] = ca[k]; }
+    }
+    wsync();
+  }
+  // local body force: cinert*cacc + cvel x* (cinert*cvel), written over cacc
+  for (int b = 1 + lane; b < m.nbody; b += 64) {
+    float f[6], t1[6], t2[6];
+    mul_inert_vec(f, s.cinert[b], cacc[b]);
+    mul_inert_vec(t1, s.cinert[b], cvel[b]);
+    cross_force(t2, cvel[b], t1);
+    for (int k = 0; k < 6; k++) f[k] += t2[k];
+    // each lane reads and writes only its own body -> in place is safe
+    for (int k = 0; k < 6; k++) cacc[b][k] = f[k];
+  }
+  wsync();
+  // subtree sum (DFS range) -> cvel storage (cvel no longer needed)
+  float sub[6];
+  const int bb = lane < m.nbody ? lane : 0;
+  for (int k = 0; k < 6; k++) sub[k] = 0;
+  if (lane < m.nbody && lane > 0)
+    for (int d = bb; d < m.body_subtree_end[bb]; d++)
+      for (int k = 0; k < 6; k++) sub[k] += cacc[d][k];
+  wsync();
+  if (lane < m.nbody)
+    for (int k = 0; k < 6; k++) cvel[bb][k] = sub[k];
+  wsync();
+  if (lane < m.nv) {
+    int j = lane;
+    float bias = dot6(s.cdof[j], cvel[m.dof_bodyid[j]]);
+    float pas = (m.disableflags & DSBL_PASSIVE) ? 0.f : -m.dof_damping[j] * s.qvel[j];
+    float act = 0.f;
+    int u = m.dof_act[j];
+    if (u >= 0 && !(m.disableflags & DSBL_ACTUATION)) {
+      float ctrl = s.ctrl[u];
+      if (m.act_ctrllimited[u] && !(m.disableflags & DSBL_CLAMPCTRL))
+        ctrl = clampf(ctrl, m.act_ctrlrange[2 * u], m.act_ctrlrange[2 * u + 1]);
+      float gear = m.act_gear[u];
+      float len = gear * s.qpos[j], vel = gear * s.qvel[j];
+      const float* bp = &m.act_bias[3 * u];
+      float f = m.act_gain[u] * ctrl + bp[0] + bp[1] * len + bp[2] * vel;
+      if (m.act_forcelimited[u]) f = clampf(f, m.act_forcerange[2 * u], m.act_forcerange[2 * u + 1]);
+      act = gear * f;
+    }
+    s.qfrc_smooth[j] = pas - bias + act;
+  }
+  wsync();
+}
+
+}  // namespace aw

@@ -1,0 +1,654 @@
+// aw_solver.h -- constraint assembly, Newton solver, noslip, touch sensor, Euler (fp32).
+//
+// Restates MuJoCo 2.1 mj_makeConstraint / mj_makeImpedance / mj_solNewton / mj_solNoSlip /
+// mj_Euler (fp64 statement: oracle/solver.cc, oracle/mjstep.cc).  Layout on the wave:
+//   * rows [0, nsparse): frictionloss / joint-limit / tendon-limit rows with <= 2 nonzeros,
+//     kept as (index, value) pairs; rows [nsparse, nefc): contact rows, dense J in LDS.
+//   * Newton: lane i holds row i of H = M + J'DJ in VGPRs; H is factored in registers
+//     (v_readlane broadcasts), the factor is written once to LDS for the backward solve.
+//   * rows are evaluated lane-per-row (two rows per lane, nefc <= 128); the exact line search
+//     and the cost are wave reductions.
+//   * noslip: lane k holds row k of inv(M) and of X = inv(M) J_edges' (<= 64 edges) in VGPRs,
+//     so each PGS update is a handful of broadcasts + one FMA per lane; qacc is kept current
+//     instead of a dual residual matrix.
+#pragma once
+#include "aw_common.h"
+
+namespace aw {
+
+// ---------------------------------------------------------------------------------------
+// dense Cholesky of a lane-distributed SPD matrix (lane i holds row i; lower part used)
+template <int NV>
+__device__ __forceinline__ void chol_factor(float (&row)[NV], int lane, float& invd) {
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    float djj = rlane(row[j], j);
+    float sq = sqrtf(fmaxf(djj, MINVAL));
+    float inv = 1.0f / sq;
+    if (lane == j) { row[j] = sq; invd = inv; }
+    else if (lane > j) row[j] *= inv;
+#pragma unroll
+    for (int k = j + 1; k < NV; k++) {
+      float lkj = rlane(row[j], k);
+      if (lane >= k) row[k] = fmaf(-row[j], lkj, row[k]);
+    }
+  }
+}
+template <int NV>
+__device__ __forceinline__ void chol_store(const float (&row)[NV], int lane, Env& s) {
+  if (lane < NV) {
+#pragma unroll
+    for (int k = 0; k < NV; k++)
+      if (k <= lane) s.L[lane][k] = row[k];
+  }
+}
+// x = inv(L L') b, b lane-distributed; L rows in registers (forward) and in LDS (backward)
+template <int NV>
+__device__ __forceinline__ float chol_solve(const float (&row)[NV], float invd, float b, int lane, const Env& s) {
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    float yj = rlane(b, j) * rlane(invd, j);
+    if (lane == j) b = yj;
+    else if (lane > j) b = fmaf(-row[j], yj, b);
+  }
+#pragma unroll
+  for (int j = NV - 1; j >= 0; j--) {
+    float xj = rlane(b, j) * rlane(invd, j);
+    if (lane == j) b = xj;
+    else if (lane < j) b = fmaf(-s.L[j][lane], xj, b);
+  }
+  return lane < NV ? b : 0.f;
+}
+// y = M x with M lane-distributed rows and x lane-distributed
+template <int NV>
+__device__ __forceinline__ float matvec(const float (&row)[NV], float x) {
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; k++) acc = fmaf(row[k], rlane(x, k), acc);
+  return acc;
+}
+
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ float getimpedance(const float* solimp, float pm) {
+  float d0 = clampf(solimp[0], 0.0001f, 0.9999f), dmax = clampf(solimp[1], 0.0001f, 0.9999f);
+  if (d0 == dmax || solimp[2] <= MINVAL) return 0.5f * (d0 + dmax);
+  float x = fabsf(pm / solimp[2]);
+  if (x >= 1 || x <= 0) return x >= 1 ? dmax : d0;
+  float y, mid = solimp[3], p = solimp[4];
+  if (p == 1) y = x;
+  else if (x <= mid) y = powf(x, p) / powf(mid, p - 1);
+  else y = 1 - powf(1 - x, p) / powf(1 - mid, p - 1);
+  return d0 + y * (dmax - d0);
+}
+
+// J_r . x  (x in LDS)
+template <int NV>
+__device__ __forceinline__ float row_dot(const Env& s, int r, const float* x) {
+  if (r < s.nsparse) {
+    int i1 = s.efc_i1[r];
+    return s.efc_v0[r] * x[s.efc_i0[r]] + (i1 >= 0 ? s.efc_v1[r] * x[i1] : 0.f);
+  }
+  const float* J = s.J[r - s.nsparse];
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; k++) acc = fmaf(J[k], x[k], acc);
+  return acc;
+}
+
+// out_k = (J' f)_k for k = lane; f given per row in s.rowbuf (must be written + synced)
+template <int NV>
+__device__ float jt_mul(Env& s, int lane) {
+  if (lane < NV) s.vec2[lane] = 0.f;
+  wsync();
+  for (int r = lane; r < s.nsparse; r += 64) {
+    float f = s.rowbuf[r];
+    if (f != 0.f) {
+      atomicAdd(&s.vec2[s.efc_i0[r]], s.efc_v0[r] * f);
+      int i1 = s.efc_i1[r];
+      if (i1 >= 0) atomicAdd(&s.vec2[i1], s.efc_v1[r] * f);
+    }
+  }
+  wsync();
+  const int li = lane < NV ? lane : NV - 1;
+  float out = s.vec2[li];
+  for (int d = 0; d < s.ndense; d++) out = fmaf(s.J[d][li], s.rowbuf[s.nsparse + d], out);
+  return lane < NV ? out : 0.f;
+}
+
+// ---------------------------------------------------------------------------------------
+// mj_makeConstraint + mj_makeImpedance + reference acceleration
+template <int NV>
+__device__ void stage_constraints(const DModel& m, Env& s, int lane) {
+  if (m.disableflags & DSBL_CONSTRAINT) {
+    if (lane == 0) { s.nefc = s.nsparse = s.ndense = 0; }
+    wsync();
+    return;
+  }
+  const int nfl = (m.disableflags & DSBL_FRICTIONLOSS) ? 0 : m.nfl;
+  // frictionloss rows (dof order)
+  if (lane < nfl) {
+    int d = m.fl_dof[lane];
+    s.efc_type[lane] = C_FRIC_DOF; s.efc_id[lane] = d;
+    s.efc_i0[lane] = d; s.efc_i1[lane] = -1; s.efc_v0[lane] = 1.f; s.efc_v1[lane] = 0.f;
+    s.efc_pm[lane] = 0.f; s.efc_floss[lane] = m.dof_frictionloss[d]; s.efc_dA[lane] = m.dof_invweight0[d];
+  }
+  // joint limits: lower then upper per joint, joints in order
+  const bool lim = !(m.disableflags & DSBL_LIMIT);
+  int lo = 0, hi = 0;
+  float dlo = 0, dhi = 0, mg = 0;
+  if (lim && lane < m.njnt && m.jnt_limited[lane]) {
+    float q = s.qpos[lane];
+    mg = m.jnt_margin[lane];
+    dlo = q - m.jnt_range[2 * lane];
+    dhi = m.jnt_range[2 * lane + 1] - q;
+    lo = dlo < mg; hi = dhi < mg;
+  }
+  int njl;
+  int off = nfl + wave_excl_scan(lo + hi, lane, &njl);
+  if (lo || hi) {
+    for (int side = 0; side < 2; side++) {
+      if (!(side ? hi : lo)) continue;
+      int r = off++;
+      if (r >= MAXEFC) { atomicOr(&s.status, (unsigned)ST_EFC_OVERFLOW); continue; }
+      s.efc_type[r] = C_LIM_JNT; s.efc_id[r] = lane;
+      s.efc_i0[r] = lane; s.efc_i1[r] = -1; s.efc_v0[r] = side ? -1.f : 1.f; s.efc_v1[r] = 0.f;
+      s.efc_pm[r] = (side ? dhi : dlo) - mg; s.efc_floss[r] = 0.f; s.efc_dA[r] = m.dof_invweight0[lane];
+    }
+  }
+  // tendon limits
+  lo = hi = 0;
+  if (lim && lane < m.ntendon && m.ten_limited[lane]) {
+    float len = s.tlen[lane];
+    mg = m.ten_margin[lane];
+    dlo = len - m.ten_range[2 * lane];
+    dhi = m.ten_range[2 * lane + 1] - len;
+    lo = dlo < mg; hi = dhi < mg;
+  }
+  int ntl;
+  off = nfl + njl + wave_excl_scan(lo + hi, lane, &ntl);
+  if (lo || hi) {
+    for (int side = 0; side < 2; side++) {
+      if (!(side ? hi : lo)) continue;
+      int r = off++;
+      if (r >= MAXEFC) { atomicOr(&s.status, (unsigned)ST_EFC_OVERFLOW); continue; }
+      float sg = side ? -1.f : 1.f;
+      s.efc_type[r] = C_LIM_TEN; s.efc_id[r] = lane;
+      s.efc_i0[r] = m.ten_d0[lane]; s.efc_i1[r] = m.ten_d1[lane];
+      s.efc_v0[r] = sg * m.ten_c0[lane]; s.efc_v1[r] = sg * m.ten_c1[lane];
+      s.efc_pm[r] = (side ? dhi : dlo) - mg; s.efc_floss[r] = 0.f; s.efc_dA[r] = m.ten_invweight0[lane];
+    }
+  }
+  int nsparse = nfl + njl + ntl;
+  if (nsparse > MAXEFC) nsparse = MAXEFC;
+  // contacts: dense rows
+  int ncon = s.ncon;
+  int dim = 0, nr = 0, pair = 0;
+  if (lane < ncon) {
+    pair = s.con_pair[lane];
+    dim = m.cp_condim[pair];
+    nr = dim == 1 ? 1 : 2 * (dim - 1);
+  }
+  int ntot;
+  int doff = wave_excl_scan(nr, lane, &ntot);
+  bool inc = lane < ncon && doff + nr <= MAXDENSE && nsparse + doff + nr <= MAXEFC;
+  int nd = 0;
+  {
+    int cand = inc ? doff + nr : 0;
+    nd = (int)wave_max((float)cand);
+  }
+  if (lane < ncon && !inc) atomicOr(&s.status, (unsigned)ST_EFC_OVERFLOW);
+  if (lane < ncon) s.con_efc[lane] = inc ? nsparse + doff : -1;
+  if (inc) {
+    int g1 = m.cp_g1[pair], g2 = m.cp_g2[pair];
+    int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
+    float tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
+    float rot = m.body_invweight0[2 * b1 + 1] + m.body_invweight0[2 * b2 + 1];
+    float pm = s.con_dist[lane] - (m.cp_margin[pair] - m.cp_gap[pair]);
+    int r = nsparse + doff;
+    if (dim == 1) {
+      s.efc_type[r] = C_CON_FRICTIONLESS; s.efc_id[r] = lane; s.efc_pm[r] = pm; s.efc_floss[r] = 0.f;
+      s.efc_dA[r] = tran; s.efc_i0[r] = 0; s.efc_i1[r] = 0;
+    } else {
+      for (int k = 1; k < dim; k++) {
+        float fri = m.cp_friction[5 * pair + k - 1];
+        float dA = tran + fri * fri * (k < 3 ? tran : rot);
+        for (int sd = 0; sd < 2; sd++) {
+          s.efc_type[r] = C_CON_PYRAMIDAL; s.efc_id[r] = lane; s.efc_pm[r] = pm; s.efc_floss[r] = 0.f;
+          s.efc_dA[r] = dA; s.efc_i0[r] = k; s.efc_i1[r] = sd ? -1 : 1;
+          r++;
+        }
+      }
+    }
+  }
+  if (lane == 0) { s.nsparse = nsparse; s.ndense = nd; s.nefc = nsparse + nd; }
+  wsync();
+  // dense J rows: one contact at a time, lane = dof
+  for (int c = 0; c < ncon; c++) {
+    int r0 = s.con_efc[c];
+    if (r0 < 0) break;
+    int pr = s.con_pair[c];
+    int cdim = m.cp_condim[pr];
+    if (lane < NV) {
+      int k = lane;
+      int b1 = m.geom_bodyid[m.cp_g1[pr]], b2 = m.geom_bodyid[m.cp_g2[pr]];
+      const float* pos = s.con_pos[c];
+      const float* fr = s.con_frame[c];
+      const float* cd = s.cdof[k];
+      float jp[3] = {0, 0, 0}, jr[3] = {0, 0, 0};
+      if ((m.body_dofmask[b2] >> k) & 1ull) {
+        float off3[3], t[3];
+        sub3(off3, pos, s.subcom[m.body_rootid[b2]]);
+        cross3(t, cd, off3);
+        for (int q = 0; q < 3; q++) { jr[q] += cd[q]; jp[q] += cd[3 + q] + t[q]; }
+      }
+      if ((m.body_dofmask[b1] >> k) & 1ull) {
+        float off3[3], t[3];
+        sub3(off3, pos, s.subcom[m.body_rootid[b1]]);
+        cross3(t, cd, off3);
+        for (int q = 0; q < 3; q++) { jr[q] -= cd[q]; jp[q] -= cd[3 + q] + t[q]; }
+      }
+      float B[6];
+      for (int q = 0; q < 3; q++) { B[q] = dot3(fr + 3 * q, jp); B[3 + q] = dot3(fr + 3 * q, jr); }
+      int d = r0 - nsparse;
+      if (cdim == 1) {
+        s.J[d][k] = B[0];
+      } else {
+        for (int kk = 1; kk < cdim; kk++) {
+          float fri = m.cp_friction[5 * pr + kk - 1];
+          s.J[d][k] = B[0] + fri * B[kk];
+          s.J[d + 1][k] = B[0] - fri * B[kk];
+          d += 2;
+        }
+      }
+    }
+  }
+  wsync();
+  // impedance, regularisation, reference acceleration
+  for (int r = lane; r < s.nefc; r += 64) {
+    int t = s.efc_type[r], id = s.efc_id[r];
+    const float *solref, *solimp;
+    if (t == C_FRIC_DOF) { solref = &m.dof_solref[2 * id]; solimp = &m.dof_solimp[5 * id]; }
+    else if (t == C_LIM_JNT) { solref = &m.jnt_solref[2 * id]; solimp = &m.jnt_solimp[5 * id]; }
+    else if (t == C_LIM_TEN) { solref = &m.ten_solref[2 * id]; solimp = &m.ten_solimp[5 * id]; }
+    else { int pr = s.con_pair[id]; solref = &m.cp_solref[2 * pr]; solimp = &m.cp_solimp[5 * pr]; }
+    float pm = s.efc_pm[r];
+    float imp = getimpedance(solimp, pm);
+    float dmax = clampf(solimp[1], 0.0001f, 0.9999f);
+    float K, B;
+    if (solref[0] > 0) {
+      float tc = solref[0], dr = solref[1];
+      if (!(m.disableflags & DSBL_REFSAFE)) tc = fmaxf(tc, 2.f * m.timestep);
+      K = 1.f / (dmax * dmax * tc * tc * dr * dr);
+      B = 2.f / (dmax * tc);
+    } else {
+      K = -solref[0] / (dmax * dmax);
+      B = -solref[1] / dmax;
+    }
+    float R = fmaxf((1.f - imp) * s.efc_dA[r] / imp, MINVAL);
+    s.efc_D[r] = 1.f / R;
+    float vel = row_dot<NV>(s, r, s.qvel);
+    s.efc_aref[r] = -B * vel - K * imp * pm;
+  }
+  wsync();
+}
+
+// ---------------------------------------------------------------------------------------
+// Newton solver
+struct RowR {
+  float D, floss, Jaref, Jp, force;
+  int st, fr, valid;
+};
+
+__device__ __forceinline__ float row_eval(const RowR& r, float jar, float* force, int* st) {
+  if (!r.valid) { *force = 0.f; *st = S_SAT; return 0.f; }
+  if (r.fr) {
+    float f = r.floss, R = 1.f / r.D;
+    if (jar <= -R * f) { *force = f; *st = S_LNEG; return -f * jar - 0.5f * R * f * f; }
+    if (jar >= R * f) { *force = -f; *st = S_LPOS; return f * jar - 0.5f * R * f * f; }
+    *force = -r.D * jar; *st = S_QUAD; return 0.5f * r.D * jar * jar;
+  }
+  if (jar < 0) { *force = -r.D * jar; *st = S_QUAD; return 0.5f * r.D * jar * jar; }
+  *force = 0.f; *st = S_SAT; return 0.f;
+}
+
+template <int NV>
+__device__ void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[NV], float& a) {
+  const int nefc = s.nefc;
+  const float fs = lane < NV ? s.qfrc_smooth[lane] : 0.f;
+  const float a0 = lane < NV ? s.qacc_smooth[lane] : 0.f;
+  RowR rr[2];
+  for (int h = 0; h < 2; h++) {
+    int r = lane + 64 * h;
+    rr[h].valid = r < nefc;
+    int rc = rr[h].valid ? r : 0;
+    rr[h].D = s.efc_D[rc];
+    rr[h].floss = s.efc_floss[rc];
+    int t = s.efc_type[rc];
+    rr[h].fr = (t == C_FRIC_DOF || t == C_FRIC_TEN);
+    rr[h].Jaref = rr[h].Jp = rr[h].force = 0.f;
+    rr[h].st = S_SAT;
+  }
+  const float scale = 1.f / (m.meaninertia * (float)(NV > 1 ? NV : 1));
+  float Ma;
+  auto set_point = [&](float x) {
+    a = lane < NV ? x : 0.f;
+    Ma = matvec<NV>(Mrow, a);
+    if (lane < NV) s.vec[lane] = a;
+    wsync();
+    for (int h = 0; h < 2; h++) {
+      int r = lane + 64 * h;
+      if (r < nefc) rr[h].Jaref = row_dot<NV>(s, r, s.vec) - s.efc_aref[r];
+    }
+    wsync();
+  };
+  auto eval = [&]() {
+    float g = lane < NV ? (Ma - fs) * (a - a0) : 0.f;
+    float c = 0.f;
+    for (int h = 0; h < 2; h++) c += row_eval(rr[h], rr[h].Jaref, &rr[h].force, &rr[h].st);
+    return 0.5f * wave_sum(g) + wave_sum(c);
+  };
+  set_point(a0);
+  float cost = eval();
+  if (!(m.disableflags & DSBL_WARMSTART)) {
+    float aw = lane < NV ? s.warm[lane] : 0.f;
+    set_point(aw);
+    float cw = eval();
+    if (cw < cost) cost = cw;
+    else { set_point(a0); cost = eval(); }
+  }
+  auto gradient = [&]() {
+    for (int h = 0; h < 2; h++) { int r = lane + 64 * h; if (r < nefc) s.rowbuf[r] = rr[h].force; }
+    wsync();
+    float jf = jt_mul<NV>(s, lane);
+    return lane < NV ? Ma - fs - jf : 0.f;
+  };
+  float grad = gradient();
+  int iter = 0;
+  for (; iter < m.iterations; iter++) {
+    // Hessian H = M + J' D_quad J
+    for (int idx = lane; idx < NV * VS; idx += 64) (&s.L[0][0])[idx] = 0.f;
+    wsync();
+    for (int h = 0; h < 2; h++) {
+      int r = lane + 64 * h;
+      if (r >= nefc) continue;
+      float w = rr[h].st == S_QUAD ? rr[h].D : 0.f;
+      s.rowbuf[r] = w;
+      if (r < s.nsparse && w != 0.f) {
+        int i0 = s.efc_i0[r], i1 = s.efc_i1[r];
+        float v0 = s.efc_v0[r], v1 = s.efc_v1[r];
+        atomicAdd(&s.L[i0][i0], w * v0 * v0);
+        if (i1 >= 0) {
+          atomicAdd(&s.L[i0][i1], w * v0 * v1);
+          atomicAdd(&s.L[i1][i0], w * v0 * v1);
+          atomicAdd(&s.L[i1][i1], w * v1 * v1);
+        }
+      }
+    }
+    wsync();
+    float H[NV];
+    const int li = lane < NV ? lane : NV - 1;
+#pragma unroll
+    for (int k = 0; k < NV; k++) H[k] = Mrow[k] + s.L[li][k];
+    for (int d = 0; d < s.ndense; d++) {
+      float w = s.rowbuf[s.nsparse + d];
+      if (w == 0.f) continue;
+      float av = w * s.J[d][li];
+#pragma unroll
+      for (int k = 0; k < NV; k++) H[k] = fmaf(av, s.J[d][k], H[k]);
+    }
+    wsync();
+    float invd = 1.f;
+    chol_factor<NV>(H, lane, invd);
+    chol_store<NV>(H, lane, s);
+    wsync();
+    float p = -chol_solve<NV>(H, invd, grad, lane, s);
+    // exact line search on the piecewise-quadratic 1-D cost
+    float Mp = matvec<NV>(Mrow, p);
+    float c0 = wave_sum(lane < NV ? p * (Ma - fs) : 0.f);
+    float c1 = wave_sum(lane < NV ? p * Mp : 0.f);
+    if (lane < NV) s.vec[lane] = p;
+    wsync();
+    for (int h = 0; h < 2; h++) {
+      int r = lane + 64 * h;
+      rr[h].Jp = r < nefc ? row_dot<NV>(s, r, s.vec) : 0.f;
+    }
+    wsync();
+    auto deriv = [&](float alpha, float* d1, float* d2) {
+      float g1 = 0.f, g2 = 0.f;
+      for (int h = 0; h < 2; h++) {
+        float jp = rr[h].Jp;
+        if (!rr[h].valid || jp == 0.f) continue;
+        float f;
+        int st;
+        row_eval(rr[h], rr[h].Jaref + alpha * jp, &f, &st);
+        g1 -= f * jp;
+        if (st == S_QUAD) g2 += rr[h].D * jp * jp;
+      }
+      *d1 = c0 + alpha * c1 + wave_sum(g1);
+      *d2 = c1 + wave_sum(g2);
+    };
+    float d1, d2;
+    deriv(0.f, &d1, &d2);
+    float alpha = 0.f;
+    if (d1 < 0.f) {
+      float tol = 1e-6f * fabsf(d1), lo = 0.f, hi = -1.f;
+      for (int it = 0; it < 50; it++) {
+        float an = alpha - d1 / d2;
+        if (hi >= 0.f && (an <= lo || an >= hi)) an = 0.5f * (lo + hi);
+        if (an == alpha) break;
+        alpha = an;
+        deriv(alpha, &d1, &d2);
+        if (d1 < 0.f) lo = alpha; else hi = alpha;
+        if (fabsf(d1) <= tol) break;
+      }
+    }
+    if (alpha == 0.f) { iter++; break; }
+    a += alpha * p;
+    Ma += alpha * Mp;
+    for (int h = 0; h < 2; h++) rr[h].Jaref += alpha * rr[h].Jp;
+    float oldcost = cost;
+    cost = eval();
+    grad = gradient();
+    float gn = sqrtf(wave_sum(grad * grad));
+    float improvement = scale * (oldcost - cost), gradnorm = scale * gn;
+    if (improvement < m.tolerance || gradnorm < m.tolerance) { iter++; break; }
+  }
+  for (int h = 0; h < 2; h++) {
+    int r = lane + 64 * h;
+    if (r < nefc) s.efc_force[r] = rr[h].force;
+  }
+  wsync();
+}
+
+// ---------------------------------------------------------------------------------------
+// noslip: PGS over frictionloss rows and opposing pyramid-edge pairs, no regularisation
+template <int NV>
+__device__ void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[NV], float& qacc) {
+  const int nsparse = s.nsparse, ndense = s.ndense;
+  // inv(M): factor, then lane i solves M x = e_i (multi-RHS, L entries broadcast from LDS)
+  float row[NV];
+#pragma unroll
+  for (int k = 0; k < NV; k++) row[k] = Mrow[k];
+  float invd = 1.f;
+  chol_factor<NV>(row, lane, invd);
+  chol_store<NV>(row, lane, s);
+  if (lane < NV) s.vec2[lane] = invd;
+  wsync();
+  float Mi[NV];
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    float acc = (j == lane) ? 1.f : 0.f;
+#pragma unroll
+    for (int k = 0; k < j; k++) acc = fmaf(-s.L[j][k], Mi[k], acc);
+    Mi[j] = acc * s.vec2[j];
+  }
+#pragma unroll
+  for (int j = NV - 1; j >= 0; j--) {
+    float acc = Mi[j];
+#pragma unroll
+    for (int k = j + 1; k < NV; k++) acc = fmaf(-s.L[k][j], Mi[k], acc);
+    Mi[j] = acc * s.vec2[j];
+  }
+  if (lane >= NV) {
+#pragma unroll
+    for (int k = 0; k < NV; k++) Mi[k] = 0.f;
+  }
+  // X[e] = (inv(M) J_e')_lane for pyramidal dense rows
+  float X[MAXDENSE];
+#pragma unroll
+  for (int e = 0; e < MAXDENSE; e++) {
+    float acc = 0.f;
+    if (e < ndense && s.efc_type[nsparse + e] == C_CON_PYRAMIDAL) {
+#pragma unroll
+      for (int j = 0; j < NV; j++) acc = fmaf(Mi[j], s.J[e][j], acc);
+    }
+    X[e] = acc;
+  }
+  const int li = lane < NV ? lane : 0;
+  const float lm = lane < NV ? 1.f : 0.f;
+  // pair constants A11, A22, A12
+#pragma unroll
+  for (int e = 0; e + 1 < MAXDENSE; e++) {
+    if (e < ndense - 1 && s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1) {
+      float j1 = lm * s.J[e][li], j2 = lm * s.J[e + 1][li];
+      float a11 = wave_sum(j1 * X[e]), a22 = wave_sum(j2 * X[e + 1]), a12 = wave_sum(j1 * X[e + 1]);
+      if (lane == 0) { s.ns_a[e][0] = a11; s.ns_a[e][1] = a22; s.ns_a[e][2] = a12; }
+    }
+  }
+  // forces: frictionloss rows per dof lane, dense rows per lane
+  float ffl = 0.f, fd = 0.f;
+  if (lane < NV && m.fl_row[lane] >= 0 && m.fl_row[lane] < nsparse) ffl = s.efc_force[m.fl_row[lane]];
+  if (lane < ndense) fd = s.efc_force[nsparse + lane];
+  wsync();
+  qacc = lane < NV ? qacc : 0.f;
+  const float scale = 1.f / (m.meaninertia * (float)(NV > 1 ? NV : 1));
+  const bool use_fl = !(m.disableflags & DSBL_FRICTIONLOSS);
+  for (int it = 0; it < m.noslip_iterations; it++) {
+    float impr = 0.f;
+#pragma unroll
+    for (int d = 0; d < NV; d++) {
+      int row = m.fl_row[d];
+      if (!use_fl || row < 0 || row >= nsparse) continue;
+      float Add = rlane(Mi[d], d);
+      if (Add < MINVAL) continue;
+      float r = rlane(qacc, d) - s.efc_aref[row];
+      float f = rlane(ffl, d), fl = s.efc_floss[row];
+      float x = clampf(f - r / Add, -fl, fl);
+      float delta = x - f;
+      if (delta == 0.f) continue;
+      impr -= r * delta + 0.5f * Add * delta * delta;
+      qacc = fmaf(Mi[d], delta, qacc);
+      if (lane == d) ffl = x;
+    }
+#pragma unroll
+    for (int e = 0; e + 1 < MAXDENSE; e++) {
+      if (!(e < ndense - 1 && s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1)) continue;
+      float A11 = s.ns_a[e][0], A22 = s.ns_a[e][1], A12 = s.ns_a[e][2];
+      float K = A11 + A22 - 2.f * A12;
+      if (K < MINVAL) continue;
+      float r1 = wave_sum(lm * s.J[e][li] * qacc) - s.efc_aref[nsparse + e];
+      float r2 = wave_sum(lm * s.J[e + 1][li] * qacc) - s.efc_aref[nsparse + e + 1];
+      float f1 = rlane(fd, e), f2 = rlane(fd, e + 1);
+      float sum = f1 + f2, x = f1 - f2;
+      float xn = clampf(x - 2.f * (r1 - r2) / K, -sum, sum);
+      float d1 = 0.5f * (sum + xn) - f1, d2 = 0.5f * (sum - xn) - f2;
+      if (d1 == 0.f && d2 == 0.f) continue;
+      impr -= r1 * d1 + r2 * d2 + 0.5f * (A11 * d1 * d1 + 2.f * A12 * d1 * d2 + A22 * d2 * d2);
+      qacc = fmaf(X[e], d1, fmaf(X[e + 1], d2, qacc));
+      if (lane == e) fd = f1 + d1;
+      if (lane == e + 1) fd = f2 + d2;
+    }
+    if (impr * scale < m.noslip_tolerance) break;
+  }
+  if (lane < NV && m.fl_row[lane] >= 0 && m.fl_row[lane] < nsparse) s.efc_force[m.fl_row[lane]] = ffl;
+  if (lane < ndense) s.efc_force[nsparse + lane] = fd;
+  wsync();
+}
+
+// ---------------------------------------------------------------------------------------
+// mju_rayGeom for site shapes: distance to the first crossing at t >= 0, or -1
+__device__ float ray_geom(const float* pos, const float* mat, const float* size, const float* pnt,
+                          const float* vec, int type) {
+  float dif[3], lp[3], lv[3];
+  sub3(dif, pnt, pos);
+  mulmtv3(lp, mat, dif);
+  mulmtv3(lv, mat, vec);
+  float best = -1.f;
+  auto consider = [&](float t) { if (t >= 0 && (best < 0 || t < best)) best = t; };
+  auto sphere = [&](float cz, float r) {
+    float o[3] = {lp[0], lp[1], lp[2] - cz};
+    float a = dot3(lv, lv), b = dot3(o, lv), cc = dot3(o, o) - r * r;
+    float disc = b * b - a * cc;
+    if (disc < 0 || a < MINVAL) return;
+    float sq = sqrtf(disc);
+    consider((-b - sq) / a);
+    consider((-b + sq) / a);
+  };
+  if (type == GEOM_SPHERE) sphere(0.f, size[0]);
+  else if (type == GEOM_BOX) {
+    for (int k = 0; k < 3; k++) {
+      if (fabsf(lv[k]) < MINVAL) continue;
+      for (int sd = -1; sd <= 1; sd += 2) {
+        float t = (sd * size[k] - lp[k]) / lv[k];
+        int u = (k + 1) % 3, v = (k + 2) % 3;
+        if (fabsf(lp[u] + t * lv[u]) <= size[u] && fabsf(lp[v] + t * lv[v]) <= size[v]) consider(t);
+      }
+    }
+  } else if (type == GEOM_CYLINDER || type == GEOM_CAPSULE) {
+    float r = size[0], h = size[1];
+    float a = lv[0] * lv[0] + lv[1] * lv[1];
+    float b = lp[0] * lv[0] + lp[1] * lv[1];
+    float cc = lp[0] * lp[0] + lp[1] * lp[1] - r * r;
+    float disc = b * b - a * cc;
+    if (a > MINVAL && disc >= 0) {
+      float sq = sqrtf(disc);
+      for (int sd = -1; sd <= 1; sd += 2) {
+        float t = (-b + sd * sq) / a;
+        if (fabsf(lp[2] + t * lv[2]) <= h) consider(t);
+      }
+    }
+    if (type == GEOM_CYLINDER) {
+      if (fabsf(lv[2]) > MINVAL)
+        for (int sd = -1; sd <= 1; sd += 2) {
+          float t = (sd * h - lp[2]) / lv[2];
+          float px = lp[0] + t * lv[0], py = lp[1] + t * lv[1];
+          if (px * px + py * py <= r * r) consider(t);
+        }
+    } else {
+      sphere(h, r);
+      sphere(-h, r);
+    }
+  }
+  return best;
+}
+
+// touch sensors of the task (mj_sensorAcc, mjSENS_TOUCH)
+__device__ void stage_touch(const DModel& m, Env& s, int lane) {
+  for (int t = 0; t < m.ntouch; t++) {
+    int site = m.touch_site[t], bid = m.site_bodyid[site];
+    float val = 0.f;
+    if (lane < s.ncon && s.con_efc[lane] >= 0 && !(m.disableflags & DSBL_SENSOR)) {
+      int pr = s.con_pair[lane];
+      int b1 = m.geom_bodyid[m.cp_g1[pr]], b2 = m.geom_bodyid[m.cp_g2[pr]];
+      if (bid == b1 || bid == b2) {
+        int adr = s.con_efc[lane], dim = m.cp_condim[pr];
+        float fn = 0.f;
+        if (dim == 1) fn = s.efc_force[adr];
+        else for (int j = 0; j < 2 * (dim - 1); j++) fn += s.efc_force[adr + j];
+        if (fn > 0.f) {
+          float ray[3];
+          copy3(ray, s.con_frame[lane]);
+          normalize3(ray);
+          if (bid == b2) scl3(ray, ray, -1.f);
+          if (ray_geom(s.sxpos[site], s.txmat[t], &m.touch_size[3 * t], s.con_pos[lane], ray, m.touch_type[t]) >= 0.f)
+            val = fn;
+        }
+      }
+    }
+    float tot = wave_sum(val);
+    if (lane == 0) s.touch[t] = tot;
+  }
+  wsync();
+}
+
+}  // namespace aw

@@ -207,8 +207,12 @@ def attach_task(model, env_id: str, variation_type: Optional[str] = None):
     m.arrays["task_param_obj"] = np.array([o for _, o, _ in lay], np.int32)
     m.arrays["task_param_comp"] = np.array([c for _, _, c in lay], np.int32)
     m.arrays["task_param_default"] = default_params(env_id, model, variation_type)
+    rr = reset_ranges(env_id, variation_type)
+    m.arrays["task_draw_lo"] = np.array([r[0] for r in rr])
+    m.arrays["task_draw_hi"] = np.array([r[1] for r in rr])
+    var = {None: 0, "mass": 1, "pos": 2, "size": 3}[variation_type]
     m.dims.update(task_kind=spec.kind, task_frame_skip=spec.frame_skip, task_horizon=spec.horizon,
-                  task_obs_dim=spec.obs_dim, task_nparam=len(lay))
+                  task_obs_dim=spec.obs_dim, task_nparam=len(lay), task_variation=var)
     if env_id == "pen-v0":
         pl, tl = pen_lengths(model)
         m.opt.update(task_pen_length=pl, task_tar_length=tl)

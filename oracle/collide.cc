@@ -12,8 +12,8 @@
  *     analytic, as the corresponding mjc_* routines;
  *   capsule-box: exact minimum of the signed distance along the axis (golden section) plus
  *     the far endpoint as second contact when within margin (MuJoCo 2.1: analytic, <= 2);
- *   box-box: separating-axis test + Sutherland-Hodgman clipping of the incident face (<= 8)
- *     or one edge-edge contact;
+ *   box-box: separating-axis test; face case -> fixed-order candidate points (incident
+ *     corners, projected reference corners, edge crossings; <= 8), edge case -> 1 contact;
  *   any pair with a cylinder (and sphere-cylinder): MPR, restating libccd's
  *     ccdMPRPenetration as used by mjc_Convex (1 contact, support inflated by margin/2).
  */
@@ -26,6 +26,7 @@
 namespace orc {
 
 static const num MINVAL = 1e-15;
+static const int MAXPAIRCON = 8;
 
 struct GeomView {
   const num* pos;
@@ -286,7 +287,10 @@ static int sphere_box(const GeomView& g1, const GeomView& g2, num margin, Contac
   return sphere_box_pt(g1.pos, g1.size[0], g2, margin, c);
 }
 
-/* box-box: SAT over 15 axes, face clipping or edge-edge */
+/* box-box: SAT over 15 axes; face contact -> candidate points in fixed order
+ * (incident-face corners inside the reference rectangle, reference corners projected onto
+ * the incident face, incident-edge x reference-edge crossings), keep depth <= margin, at most
+ * MAXPAIRCON; edge-edge -> one contact at the closest points of the two edges. */
 static int box_box(const GeomView& A, const GeomView& B, num margin, Contact* c) {
   num a[3][3], b[3][3], t[3];
   for (int k = 0; k < 3; k++) { axis_of(a[k], A.mat, k); axis_of(b[k], B.mat, k); }
@@ -311,8 +315,7 @@ static int box_box(const GeomView& A, const GeomView& B, num margin, Contact* c)
     num tl = dot3(t, L);
     num sep = std::fabs(tl) - ra - rb;
     if (sep > margin) return 0;
-    /* prefer face axes: an edge axis must be clearly better */
-    num bias = k < 6 ? 0 : 1e-6;
+    num bias = k < 6 ? 0 : 1e-6;   /* prefer face axes */
     if (sep > best + bias) {
       best = sep; bestk = k;
       copy3(bestn, L);
@@ -321,7 +324,6 @@ static int box_box(const GeomView& A, const GeomView& B, num margin, Contact* c)
   }
   if (bestk < 0) return 0;
   if (bestk < 6) {
-    /* face contact: reference box R with face normal nr (outward, toward the other box) */
     bool refA = bestk < 3;
     const GeomView& R = refA ? A : B;
     const GeomView& I = refA ? B : A;
@@ -330,11 +332,12 @@ static int box_box(const GeomView& A, const GeomView& B, num margin, Contact* c)
     int fk = refA ? bestk : bestk - 3;
     num nr[3];
     copy3(nr, bestn);
-    if (!refA) scl3(nr, nr, -1);
-    num sgn = dot3(nr, ra[fk]) > 0 ? 1 : -1;
+    if (!refA) scl3(nr, nr, -1);        /* reference face normal, toward the incident box */
+    num sg = dot3(nr, ra[fk]) > 0 ? 1 : -1;
+    int ru = (fk + 1) % 3, rv = (fk + 2) % 3;
+    num hu = R.size[ru], hv = R.size[rv];
     num fc[3];
-    for (int k = 0; k < 3; k++) fc[k] = R.pos[k] + ra[fk][k] * sgn * R.size[fk];
-    /* incident face: most anti-parallel to nr */
+    for (int k = 0; k < 3; k++) fc[k] = R.pos[k] + ra[fk][k] * sg * R.size[fk];
     int ik = 0;
     num imin = 1e300, isg = 1;
     for (int k = 0; k < 3; k++) {
@@ -342,51 +345,76 @@ static int box_box(const GeomView& A, const GeomView& B, num margin, Contact* c)
       if (dd < imin) { imin = dd; ik = k; isg = 1; }
       if (-dd < imin) { imin = -dd; ik = k; isg = -1; }
     }
-    int u = (ik + 1) % 3, v = (ik + 2) % 3;
-    num poly[16][3];
-    int np = 4;
+    int iu = (ik + 1) % 3, iv = (ik + 2) % 3;
+    num inn[3], ic[3];
+    scl3(inn, ia[ik], isg);               /* incident face outward normal */
+    for (int k = 0; k < 3; k++) ic[k] = I.pos[k] + inn[k] * I.size[ik];
+    num su = I.size[iu], sv = I.size[iv];
+    /* incident corners in order around the face */
+    num P[4][3], pu[4], pv[4];
+    const num cs[4][2] = {{1, 1}, {-1, 1}, {-1, -1}, {1, -1}};
     for (int q = 0; q < 4; q++) {
-      num su = (q == 0 || q == 3) ? 1 : -1, sv = (q < 2) ? 1 : -1;
-      for (int k = 0; k < 3; k++)
-        poly[q][k] = I.pos[k] + ia[ik][k] * isg * I.size[ik] + ia[u][k] * su * I.size[u] + ia[v][k] * sv * I.size[v];
-    }
-    /* clip against the 4 side planes of the reference face */
-    int ru = (fk + 1) % 3, rv = (fk + 2) % 3;
-    for (int side = 0; side < 4; side++) {
-      int ax = side < 2 ? ru : rv;
-      num s = (side & 1) ? -1 : 1;
-      num pn[3];
-      scl3(pn, ra[ax], s);
-      num off = dot3(pn, R.pos) + R.size[ax];
-      num out[16][3];
-      int no = 0;
-      for (int q = 0; q < np; q++) {
-        const num* P = poly[q];
-        const num* Q = poly[(q + 1) % np];
-        num dp = dot3(pn, P) - off, dq = dot3(pn, Q) - off;
-        if (dp <= 0) { copy3(out[no++], P); }
-        if ((dp < 0 && dq > 0) || (dp > 0 && dq < 0)) {
-          num tt = dp / (dp - dq);
-          for (int k = 0; k < 3; k++) out[no][k] = P[k] + (Q[k] - P[k]) * tt;
-          no++;
-        }
-        if (no >= 15) break;
-      }
-      np = no;
-      memcpy(poly, out, sizeof(num) * 3 * no);
-      if (np == 0) return 0;
+      for (int k = 0; k < 3; k++) P[q][k] = ic[k] + ia[iu][k] * cs[q][0] * su + ia[iv][k] * cs[q][1] * sv;
+      num dv[3];
+      sub3(dv, P[q], fc);
+      pu[q] = dot3(dv, ra[ru]);
+      pv[q] = dot3(dv, ra[rv]);
     }
     int cnt = 0;
     num normal[3];
     copy3(normal, bestn);
-    for (int q = 0; q < np && cnt < 8; q++) {
+    auto emit = [&](const num* p) {
+      if (cnt >= MAXPAIRCON) return;
       num dv[3];
-      sub3(dv, poly[q], fc);
+      sub3(dv, p, fc);
       num dist = dot3(dv, nr);
-      if (dist > margin) continue;
+      if (dist > margin) return;
       num pos[3];
-      for (int k = 0; k < 3; k++) pos[k] = poly[q][k] - nr[k] * dist / 2;
+      for (int k = 0; k < 3; k++) pos[k] = p[k] - nr[k] * dist / 2;
       set_contact(c + cnt++, dist, pos, normal);
+    };
+    /* (1) incident corners inside the reference rectangle */
+    for (int q = 0; q < 4; q++)
+      if (std::fabs(pu[q]) <= hu && std::fabs(pv[q]) <= hv) emit(P[q]);
+    /* (2) reference corners inside the incident face (projected along nr) */
+    num den = dot3(nr, inn);
+    if (std::fabs(den) > 1e-12) {
+      for (int q = 0; q < 4; q++) {
+        num Q[3], dq[3];
+        for (int k = 0; k < 3; k++) Q[k] = fc[k] + ra[ru][k] * cs[q][0] * hu + ra[rv][k] * cs[q][1] * hv;
+        sub3(dq, ic, Q);
+        num tt = dot3(dq, inn) / den;
+        num Qp[3];
+        for (int k = 0; k < 3; k++) Qp[k] = Q[k] + nr[k] * tt;
+        sub3(dq, Qp, ic);
+        if (std::fabs(dot3(dq, ia[iu])) <= su && std::fabs(dot3(dq, ia[iv])) <= sv) emit(Qp);
+      }
+    }
+    /* (3) incident edges crossing the reference rectangle's edge lines */
+    for (int q = 0; q < 4; q++) {
+      int q2 = (q + 1) & 3;
+      num du = pu[q2] - pu[q], dv = pv[q2] - pv[q];
+      for (int side = 0; side < 4; side++) {
+        num tt;
+        if (side < 2) {
+          num U = side == 0 ? hu : -hu;
+          if (std::fabs(du) < 1e-12) continue;
+          tt = (U - pu[q]) / du;
+          if (!(tt > 0 && tt < 1)) continue;
+          num vv = pv[q] + tt * dv;
+          if (std::fabs(vv) > hv) continue;
+        } else {
+          num V = side == 2 ? hv : -hv;
+          if (std::fabs(dv) < 1e-12) continue;
+          tt = (V - pv[q]) / dv;
+          if (!(tt > 0 && tt < 1)) continue;
+          num uu = pu[q] + tt * du;
+          if (std::fabs(uu) > hu) continue;
+        }
+        num X[3];
+        for (int k = 0; k < 3; k++) X[k] = P[q][k] + (P[q2][k] - P[q][k]) * tt;
+        emit(X);
+      }
     }
     return cnt;
   }

@@ -1,0 +1,105 @@
+"""Stage-by-stage GPU vs oracle comparison + a quick timing (diagnostic, run via gpurun)."""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+from mj_envs_amd import _native  # noqa: E402
+from mj_envs_amd.tasks import attach_task, load_model, sample_params  # noqa: E402
+from oracle.pyoracle import Oracle  # noqa: E402
+
+
+def rel(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return float(np.abs(a - b).max() / (np.abs(b).max() + 1e-12)) if a.size else 0.0
+
+
+def check(env, n=4, steps=3, dsbl=0):
+    m = attach_task(load_model(env), env)
+    blob = m.to_blob()
+    sim = _native.Sim(blob, n)
+    orc = Oracle(blob)
+    sim.set_option(disableflags=dsbl)
+    orc.set_option(disableflags=dsbl, max_con=32, max_efc=128)
+    params = sample_params(env, m, np.random.default_rng(0), n)
+    pt = torch.tensor(params, dtype=torch.float32, device="cuda")
+    obs = sim.empty(n, sim.obs_dim)
+    sim.reset(obs, params=pt)
+    st, obs_ref = orc.reset(params)
+    torch.cuda.synchronize()
+    print(f"== {env} dsbl={dsbl}: reset obs rel err {rel(obs.cpu().numpy(), obs_ref):.2e}")
+    rng = np.random.default_rng(1)
+    for k in range(steps):
+        # compare forward internals at the current (identical) state, ctrl = 0
+        qpos = torch.tensor(st["qpos"], dtype=torch.float32, device="cuda")
+        qvel = torch.tensor(st["qvel"], dtype=torch.float32, device="cuda")
+        warm = torch.tensor(st["warm"], dtype=torch.float32, device="cuda")
+        sim.set_state(qpos, qvel, warm, pt)
+        d = sim.forward_dump(0)
+        orc.forward1(params[0], st["qpos"][0], st["qvel"][0], st["warm"][0])
+        sc = orc.get("scalars")
+        print(f"  step {k}: ncon gpu/orc {d['ncon']}/{int(sc[0])} nefc {d['nefc']}/{int(sc[1])} "
+              f"xpos {rel(d['xpos'], orc.get('xpos').reshape(-1, 3)):.1e} "
+              f"M {rel(d['qM'], orc.get('qM').reshape(sim.nv, sim.nv)):.1e} "
+              f"qacc_smooth {rel(d['qacc_smooth'], orc.get('qacc_smooth')):.1e} "
+              f"qacc {rel(d['qacc'], orc.get('qacc')):.1e} "
+              f"qfrc_con {rel(d['qfrc_constraint'], orc.get('qfrc_constraint')):.1e} "
+              f"touch {d['touch']:.3f}/{orc.get('sensordata')[0]:.3f}")
+        if d["ncon"] != int(sc[0]):
+            oc = orc.get("contact").reshape(-1, 23)
+            print("   gpu con", d["con_pair"], np.round(d["con_dist"], 5))
+            print("   orc con", oc[:, 13:15].astype(int).tolist(), np.round(oc[:, 0], 5))
+        act = rng.uniform(-1, 1, (n, sim.nu))
+        at = torch.tensor(act, dtype=torch.float32, device="cuda")
+        rew = sim.empty(n)
+        dn = sim.empty(n, dtype=torch.uint8)
+        gl = sim.empty(n, dtype=torch.uint8)
+        sim.set_state(qpos, qvel, warm, pt)
+        sim.step(at, obs, rew, dn, gl)
+        o_ref, r_ref, _, _, _ = orc.step(st, act)
+        q2 = sim.empty(n, sim.nq)
+        v2 = sim.empty(n, sim.nv)
+        sim.get_state(q2, v2)
+        torch.cuda.synchronize()
+        print(f"    env-step: qpos {rel(q2.cpu().numpy(), st['qpos']):.2e} qvel {rel(v2.cpu().numpy(), st['qvel']):.2e} "
+              f"obs {rel(obs.cpu().numpy(), o_ref):.2e} reward {rel(rew.cpu().numpy(), r_ref):.2e}")
+
+
+def timing(env, n, steps=10):
+    m = attach_task(load_model(env), env)
+    sim = _native.Sim(m.to_blob(), n)
+    obs = sim.empty(n, sim.obs_dim)
+    act = sim.empty(n, sim.nu)
+    rew = sim.empty(n)
+    dn = sim.empty(n, dtype=torch.uint8)
+    gl = sim.empty(n, dtype=torch.uint8)
+    sim.reset(obs, seed=1)
+    for k in range(2):
+        sim.random_actions(act, 0, k)
+        sim.step(act, obs, rew, dn, gl, autoreset=True)
+    torch.cuda.synchronize()
+    t = time.time()
+    for k in range(steps):
+        sim.random_actions(act, 0, k)
+        sim.step(act, obs, rew, dn, gl, autoreset=True)
+    torch.cuda.synchronize()
+    dt = (time.time() - t) / steps
+    print(f"timing {env} n={n}: {dt * 1e3:.2f} ms/step -> {n / dt:.3e} env-steps/s; "
+          f"finite {bool(torch.isfinite(obs).all())}", flush=True)
+
+
+if __name__ == "__main__":
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which in ("all", "parity"):
+        check("hammer-v0", dsbl=1)          # constraints off: smooth dynamics only
+        check("hammer-v0")
+        for e in ("door-v0", "pen-v0", "relocate-v0"):
+            check(e, steps=2)
+    if which in ("all", "timing"):
+        timing("hammer-v0", 1024, 5)
+        timing("hammer-v0", 8192, 5)
+        timing("hammer-v0", 65536, 3)
