@@ -1,0 +1,181 @@
+"""Headline benchmark: hammer-v0 env-steps/s on N MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs-per-gpu E]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A "step" = one env-step of every env on every GPU: i.i.d. U(-1,1) actions from Philox
+(seed 0, counter (env, step)), 5 physics substeps (frame_skip) + reward + obs, auto-reset at
+the 200-step horizon inside the timed region, and at every episode boundary an RCCL all-gather
+of the per-env episode returns / goal counts over xGMI.  Weak scaling: envs per GPU fixed
+(default 65 536 = the north-star configuration).  Inputs are resident in HBM; value is
+whole-job env-steps/s = N * envs_per_gpu * K / max-over-ranks wall time.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+ENV_ID = "hammer-v0"
+
+
+def cpu_baseline(model_blob, env_id, budget_s=12.0):
+    """Oracle (fp64 restatement, OpenMP over envs) on the host cores: bounded sample."""
+    import numpy as np
+    from mj_envs_amd.tasks import attach_task, load_model, sample_params
+    from oracle.pyoracle import Oracle, build
+    build()
+    m = attach_task(load_model(env_id), env_id)
+    o = Oracle(model_blob)
+    o.set_option(max_con=32, max_efc=128)
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = max(1, min(threads, 16))
+    n = 64 * threads
+    rng = np.random.default_rng(0)
+    P = sample_params(env_id, m, rng, n)
+    st, _ = o.reset(P, nthreads=threads)
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        o.step(st, rng.uniform(-1, 1, (n, o.nu)), nthreads=threads)
+        steps += 1
+    dt = time.perf_counter() - t0
+    return dict(value=n * steps / dt, unit="env-steps/s", cores=threads, kind="port",
+                sample=f"{env_id}, {n} envs x {steps} env-steps (random policy), fp64 C++ oracle "
+                       f"(restated mj_step + task layer), OpenMP {threads} threads, {dt:.1f} s")
+
+
+def pmc_traffic(env_per_launch):
+    """HBM bytes per k_step launch from the committed rocprofv3 --pmc summary, or None."""
+    path = os.path.join(REPO, "profiles", "r01_pmc_kstep.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("envs") != env_per_launch:
+            return None
+        return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--envs-per-gpu", type=int, default=65536)
+    ap.add_argument("--env", default=ENV_ID)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from mj_envs_amd import _native, perfmodel
+    from mj_envs_amd.tasks import attach_task, load_model
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    env_id = args.env
+    m = attach_task(load_model(env_id), env_id)
+    blob = m.to_blob()
+    n = args.envs_per_gpu
+    sim = _native.Sim(blob, n, device=local)
+    obs = sim.empty(n, sim.obs_dim)
+    act = sim.empty(n, sim.nu)
+    rew = sim.empty(n)
+    done = sim.empty(n, dtype=torch.uint8)
+    goal = sim.empty(n, dtype=torch.uint8)
+    last_ret = sim.empty(n)
+    last_goal = sim.empty(n, dtype=torch.int32)
+    gathered_ret = sim.empty(world * n)
+    gathered_goal = sim.empty(world * n, dtype=torch.int32)
+    seed = 1 + rank                          # per-rank Philox key: global env id = (rank, env)
+    sim.reset(obs, seed=seed)
+
+    def one_step(k, ev=None):
+        sim.random_actions(act, 1000 * rank, k)
+        if ev is not None:
+            ev[0].record()
+        sim.step(act, obs, rew, done, goal, autoreset=True, seed=seed)
+        if ev is not None:
+            ev[1].record()
+        if (k + 1) % sim.horizon == 0:       # every env finished an episode this step
+            sim.episode_stats(last_ret, last_goal)
+            if world > 1:
+                dist.all_gather_into_tensor(gathered_ret, last_ret)
+                dist.all_gather_into_tensor(gathered_goal, last_goal)
+
+    for k in range(args.warmup):
+        one_step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        one_step(args.warmup + k, events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in events) / args.steps
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms = float(t[0]), float(t[1])
+    finite = bool(torch.isfinite(obs).all())
+
+    if rank == 0:
+        total_steps = world * n * args.steps
+        value = total_steps / elapsed
+        flops, counts = perfmodel.step_flops(env_id, m, sim.frame_skip)
+        achieved = flops * n / (kern_ms * 1e-3) / 1e12
+        bytes_step = perfmodel.step_bytes(sim.nq, sim.nv, sim.nu, sim.obs_dim, sim.nparam)
+        traffic = pmc_traffic(n)
+        roof = dict(bound="mfma", achieved=round(achieved, 3), peak=perfmodel.PEAK_FP32_TFLOPS,
+                    unit="TFLOP/s", frac=round(achieved / perfmodel.PEAK_FP32_TFLOPS, 5), traffic=traffic,
+                    kernel=f"k_step<{sim.nv}>", kernel_ms=round(kern_ms, 4),
+                    flops_per_env_step=round(flops), bytes_per_env_step=bytes_step,
+                    hbm_achieved_GBps=round(bytes_step * n / (kern_ms * 1e-3) / 1e9, 2),
+                    hbm_frac=round(bytes_step * n / (kern_ms * 1e-3) / 1e9 / perfmodel.PEAK_HBM_GBPS, 6),
+                    note="fp32 compute roofline (VALU == f32 MFMA peak on gfx950); FLOPs from "
+                         "perfmodel.py on profiles/work_counts_hammer.json")
+        line = dict(metric="env-steps/sec at N parallel envs, hammer-v0, 1/2/4/8 MI355X",
+                    value=round(value, 1), unit="env-steps/s", n_gpus=world, steps=args.steps,
+                    warmup=args.warmup, ms_per_step=round(elapsed / args.steps * 1e3, 4),
+                    higher_is_better=True, scaling="weak", vs_baseline=None, dtype="f32",
+                    data="synthetic (Philox U(-1,1) actions, reference reset distribution)",
+                    config=dict(workload=f"{env_id}, {n} envs per GPU (north-star config), random policy, "
+                                         f"auto-reset at horizon {sim.horizon}, RCCL all-gather of episode "
+                                         f"returns at episode ends", envs_per_gpu=n, total_envs=world * n,
+                                frame_skip=sim.frame_skip, parallelism=f"env-shard x{world}"),
+                    roofline=roof, finite=finite)
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                line["cpu_baseline"] = cpu_baseline(blob, env_id)
+            except Exception as e:  # the baseline must not hide the GPU number
+                line["cpu_baseline"] = dict(value=None, error=str(e))
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

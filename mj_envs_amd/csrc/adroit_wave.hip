@@ -31,7 +31,7 @@ struct DState {
 
 // ---------------------------------------------------------------------------------------
 // contacts -> key order (bitonic sort of (key, slot) over the wave), then frames
-__device__ void sort_contacts(Env& s, int lane) {
+AW_DEV void sort_contacts(Env& s, int lane) {
   int n = s.ncon;
   if (n > MAXCON) n = MAXCON;
   int key = lane < n ? s.con_key[lane] : 0x7fffffff;
@@ -68,18 +68,22 @@ __device__ void sort_contacts(Env& s, int lane) {
   wsync();
 }
 
-__device__ void stage_collision(const DModel& m, Env& s, int lane) {
+AW_DEV void stage_collision(const DModel& m, Env& s, int lane) {
   if (lane == 0) s.ncon = 0;
   wsync();
   if (!(m.disableflags & (DSBL_CONSTRAINT | DSBL_CONTACT)))
+    {
+#ifndef X_NOCOLL
     for (int p = lane; p < m.npairall; p += 64) collide_pair(m, s, p);
+#endif
+    }
   wsync();
   sort_contacts(s, lane);
 }
 
 // mj_forward: everything up to qacc / forces / sensors; Mrow is left in registers
 template <int NV>
-__device__ void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
+AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
   stage_kinematics(m, s, lane);
   stage_collision(m, s, lane);
   stage_com(m, s, lane);
@@ -105,8 +109,13 @@ __device__ void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
     wsync();
   } else {
     float a = 0.f;
+#ifndef X_NONEWTON
     solve_newton<NV>(m, s, lane, Mrow, a);
+#endif
+    
+#ifndef X_NONOSLIP
     if (m.noslip_iterations > 0 && !(m.disableflags & DSBL_NOSLIP)) solve_noslip<NV>(m, s, lane, Mrow, a);
+#endif
     for (int r = lane; r < s.nefc; r += 64) s.rowbuf[r] = s.efc_force[r];
     wsync();
     float qc = jt_mul<NV>(s, lane);
@@ -118,7 +127,7 @@ __device__ void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
 
 // mj_Euler: implicit joint damping, semi-implicit positions, warmstart <- qacc
 template <int NV>
-__device__ void euler(const DModel& m, Env& s, int lane, const float (&Mrow)[NV]) {
+AW_DEV void euler(const DModel& m, Env& s, int lane, const float (&Mrow)[NV]) {
   const float h = m.timestep;
   const bool dmp = !(m.disableflags & (DSBL_EULERDAMP | DSBL_PASSIVE));
   float acc;
@@ -146,38 +155,38 @@ __device__ void euler(const DModel& m, Env& s, int lane, const float (&Mrow)[NV]
 }
 
 template <int NV>
-__device__ void reset_state(Env& s, int lane) {
+AW_DEV void reset_state(Env& s, int lane) {
   if (lane < NV) { s.qpos[lane] = 0.f; s.qvel[lane] = 0.f; s.warm[lane] = 0.f; }
   wsync();
 }
 
-__device__ __forceinline__ bool bad_value(float x) { return !(fabsf(x) <= 1e10f); }
+AW_DEV bool bad_value(float x) { return !(fabsf(x) <= 1e10f); }
 
-// mj_step (Euler) with mj_checkPos / checkVel / checkAcc
+// mj_checkPos / mj_checkVel: bad state -> flag + reset to qpos0 / 0
 template <int NV>
-__device__ void substep(const DModel& m, Env& s, int lane) {
-  float Mrow[NV];
-  {
-    bool bp = lane < NV && bad_value(s.qpos[lane]);
-    bool bv = lane < NV && bad_value(s.qvel[lane]);
-    unsigned long long bpm = __ballot(bp), bvm = __ballot(bv);
-    if (bpm | bvm) {
-      if (lane == 0) s.status |= (bpm ? ST_BADQPOS : 0u) | (bvm ? ST_BADQVEL : 0u);
-      reset_state<NV>(s, lane);
-    }
+AW_DEV void check_state(Env& s, int lane) {
+  bool bp = lane < NV && bad_value(s.qpos[lane]);
+  bool bv = lane < NV && bad_value(s.qvel[lane]);
+  unsigned long long bpm = __ballot(bp), bvm = __ballot(bv);
+  if (bpm | bvm) {
+    if (lane == 0) s.status |= (bpm ? ST_BADQPOS : 0u) | (bvm ? ST_BADQVEL : 0u);
+    reset_state<NV>(s, lane);
   }
-  forward<NV>(m, s, lane, Mrow);
+}
+// mj_checkAcc: bad qacc -> flag + reset; the caller re-runs forward
+template <int NV>
+AW_DEV bool check_acc(Env& s, int lane) {
   if (__ballot(lane < NV && bad_value(s.qacc[lane]))) {
     if (lane == 0) s.status |= ST_BADQACC;
     reset_state<NV>(s, lane);
-    forward<NV>(m, s, lane, Mrow);
+    return true;
   }
-  euler<NV>(m, s, lane, Mrow);
+  return false;
 }
 
 // ---------------------------------------------------------------------------------------
 template <int NV>
-__device__ void load_env(const DModel& m, Env& s, const DState& st, int env, int lane) {
+AW_DEV void load_env(const DModel& m, Env& s, const DState& st, int env, int lane) {
   if (lane < NV) {
     s.qpos[lane] = st.qpos[(size_t)env * m.nq + lane];
     s.qvel[lane] = st.qvel[(size_t)env * m.nv + lane];
@@ -186,24 +195,24 @@ __device__ void load_env(const DModel& m, Env& s, const DState& st, int env, int
   if (lane == 0) s.status = 0u;
 }
 template <int NV>
-__device__ void store_env(const DModel& m, Env& s, const DState& st, int env, int lane) {
+AW_DEV void store_env(const DModel& m, Env& s, const DState& st, int env, int lane) {
   if (lane < NV) {
     st.qpos[(size_t)env * m.nq + lane] = s.qpos[lane];
     st.qvel[(size_t)env * m.nv + lane] = s.qvel[lane];
     st.warm[(size_t)env * m.nv + lane] = s.warm[lane];
   }
 }
-__device__ void write_obs(const DModel& m, Env& s, int lane, float* out) {
+AW_DEV void write_obs(const DModel& m, Env& s, int lane, float* out) {
   task_obs(m, s, lane, s.rowbuf);
   wsync();
   for (int o = lane; o < m.obs_dim; o += 64) out[o] = s.rowbuf[o];
   wsync();
 }
 
-// reset one env in LDS: params (given or sampled), qpos0/0/0, forward, obs
+// reset bookkeeping + parameters (given or sampled) + qpos0; forward runs in the caller
 template <int NV>
-__device__ void reset_env(const DModel& m, Env& s, const DState& st, int env, int lane,
-                          const float* params_in, uint64_t seed, float* obs) {
+AW_DEV void reset_prepare(const DModel& m, Env& s, const DState& st, int env, int lane,
+                          const float* params_in, uint64_t seed) {
   float* prm = st.params + (size_t)env * m.nparam;
   if (lane == 0) {
     if (params_in) {
@@ -211,7 +220,9 @@ __device__ void reset_env(const DModel& m, Env& s, const DState& st, int env, in
     } else {
       float tmp[MAXP];
       sample_params(m, seed, (uint32_t)env, (uint32_t)st.episode[env], tmp);
-      for (int p = 0; p < m.nparam; p++) prm[p] = tmp[p];
+#pragma unroll
+      for (int p = 0; p < MAXP; p++)
+        if (p < m.nparam) prm[p] = tmp[p];
     }
     st.ep_len[env] = 0;
     st.ep_ret[env] = 0.f;
@@ -222,11 +233,22 @@ __device__ void reset_env(const DModel& m, Env& s, const DState& st, int env, in
   if (lane < m.nu) s.ctrl[lane] = 0.f;
   reset_state<NV>(s, lane);
   stage_model(m, s, prm, lane);
+}
+
+// reset one env in LDS: params (given or sampled), qpos0/0/0, forward, obs
+template <int NV>
+AW_DEV void reset_env(const DModel& m, Env& s, const DState& st, int env, int lane,
+                      const float* params_in, uint64_t seed, float* obs) {
+  reset_prepare<NV>(m, s, st, env, lane, params_in, seed);
   float Mrow[NV];
   forward<NV>(m, s, lane, Mrow);
   if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
 }
 
+// One launch = one env-step of every env: frame_skip x (forward + Euler), task layer, and the
+// in-kernel auto-reset.  forward<NV> has exactly ONE inlined call site (the loop below drives
+// substeps, the mj_checkAcc retry and the reset forward through it), which keeps the code
+// object small enough for the instruction cache.
 template <int NV>
 __global__ void __launch_bounds__(64) k_step(DModel m, DState st, int n, const float* __restrict__ actions,
                                              float* obs, float* reward, uint8_t* done, uint8_t* goal,
@@ -240,41 +262,57 @@ __global__ void __launch_bounds__(64) k_step(DModel m, DState st, int n, const f
     s.ctrl[lane] = m.act_mid[lane] + a * m.act_rng[lane];
   }
   stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
-  for (int k = 0; k < m.frame_skip; k++) substep<NV>(m, s, lane);
+  float Mrow[NV];
   float* ob = obs + (size_t)env * m.obs_dim;
-  write_obs(m, s, lane, ob);
-  int term = 0, trunc = 0;
-  if (lane == 0) {
-    float r;
-    int dn, gl;
-    task_reward(m, s, &r, &dn, &gl);
-    reward[env] = r;
-    goal[env] = (uint8_t)gl;
-    int t = st.ep_len[env] + 1;
-    term = dn;
-    trunc = (m.horizon > 0 && t >= m.horizon) ? 1 : 0;
-    done[env] = (uint8_t)(term | (trunc << 1));
-    float ret = st.ep_ret[env] + r;
-    int gcount = st.ep_goal[env] + gl;
-    st.ep_len[env] = t;
-    st.ep_ret[env] = ret;
-    st.ep_goal[env] = gcount;
-    st.status[env] = s.status;
-    if (term || trunc) {
-      st.last_ret[env] = ret;
-      st.last_goal[env] = gcount;
-      st.last_len[env] = t;
-      st.episode[env] += 1;
+  int sub = 0;
+  bool resetting = false, retry = false;
+#pragma nounroll
+  while (true) {
+    if (!resetting && !retry) check_state<NV>(s, lane);
+    forward<NV>(m, s, lane, Mrow);
+    if (resetting) break;
+    if (!retry && check_acc<NV>(s, lane)) { retry = true; continue; }
+    retry = false;
+    euler<NV>(m, s, lane, Mrow);
+    if (++sub < m.frame_skip) continue;
+    // env-step complete: observation, reward, episode bookkeeping
+    write_obs(m, s, lane, ob);
+    int term = 0, trunc = 0;
+    if (lane == 0) {
+      float r;
+      int dn, gl;
+      task_reward(m, s, &r, &dn, &gl);
+      reward[env] = r;
+      goal[env] = (uint8_t)gl;
+      int t = st.ep_len[env] + 1;
+      term = dn;
+      trunc = (m.horizon > 0 && t >= m.horizon) ? 1 : 0;
+      done[env] = (uint8_t)(term | (trunc << 1));
+      float ret = st.ep_ret[env] + r;
+      int gcount = st.ep_goal[env] + gl;
+      st.ep_len[env] = t;
+      st.ep_ret[env] = ret;
+      st.ep_goal[env] = gcount;
+      st.status[env] = s.status;
+      if (term || trunc) {
+        st.last_ret[env] = ret;
+        st.last_goal[env] = gcount;
+        st.last_len[env] = t;
+        st.episode[env] += 1;
+      }
     }
-  }
-  store_env<NV>(m, s, st, env, lane);
-  int ended = __shfl(term | trunc, 0, 64);
-  if (autoreset && ended) {
+    store_env<NV>(m, s, st, env, lane);
+    int ended = __shfl(term | trunc, 0, 64);
+    if (!(autoreset && ended)) break;
     __threadfence_block();
     if (terminal_obs)
       for (int o = lane; o < m.obs_dim; o += 64) terminal_obs[(size_t)env * m.obs_dim + o] = s.rowbuf[o];
     wsync();
-    reset_env<NV>(m, s, st, env, lane, nullptr, seed, obs);
+    reset_prepare<NV>(m, s, st, env, lane, nullptr, seed);
+    resetting = true;
+  }
+  if (resetting) {
+    write_obs(m, s, lane, ob);
     store_env<NV>(m, s, st, env, lane);
   }
 }
@@ -678,6 +716,13 @@ static void launch_dump(aw_handle* h, int env, const float* ctrl, float* out, hi
   hipLaunchKernelGGL((k_dump<NV>), dim3(1), dim3(64), 0, st, h->m, h->st, env, ctrl, out);
 }
 
+#ifdef AW_ONLY_NV
+#define DISPATCH_NV(NVV, CALL)                                                     \
+  switch (NVV) {                                                                   \
+    case AW_ONLY_NV: CALL(AW_ONLY_NV); break;                                      \
+    default: return fail(AW_EUNSUPPORTED, "nv not instantiated in this build");   \
+  }
+#else
 #define DISPATCH_NV(NVV, CALL)                                                     \
   switch (NVV) {                                                                   \
     case 30: CALL(30); break;                                                      \
@@ -685,6 +730,7 @@ static void launch_dump(aw_handle* h, int env, const float* ctrl, float* out, hi
     case 36: CALL(36); break;                                                      \
     default: return fail(AW_EUNSUPPORTED, "nv not instantiated (30/33/36)");      \
   }
+#endif
 
 extern "C" {
 

@@ -25,9 +25,9 @@ struct Emit {
   int cnt;
 };
 
-__device__ __forceinline__ void axis_of(float* a, const float* m, int k) { a[0] = m[k]; a[1] = m[3 + k]; a[2] = m[6 + k]; }
+AW_DEV void axis_of(float* a, const float* m, int k) { a[0] = m[k]; a[1] = m[3 + k]; a[2] = m[6 + k]; }
 
-__device__ __forceinline__ void emit(Emit& e, float dist, const float* pos, const float* n) {
+AW_DEV void emit(Emit& e, float dist, const float* pos, const float* n) {
   if (e.cnt >= MAXPAIRCON) return;
   int slot = atomicAdd(&e.s->ncon, 1);
   if (slot < MAXCON) {
@@ -45,7 +45,7 @@ __device__ __forceinline__ void emit(Emit& e, float dist, const float* pos, cons
 }
 
 // ---------------------------------------------------------------------------------------
-__device__ void c_plane_sphere(const float* p1, const float* m1, const float* p2, float r, float margin, Emit& e) {
+AW_DEV void c_plane_sphere(const float* p1, const float* m1, const float* p2, float r, float margin, Emit& e) {
   float n[3], dif[3];
   axis_of(n, m1, 2);
   sub3(dif, p2, p1);
@@ -56,7 +56,7 @@ __device__ void c_plane_sphere(const float* p1, const float* m1, const float* p2
   emit(e, dist, pos, n);
 }
 
-__device__ void c_plane_capsule(const GV& a, const GV& b, float margin, Emit& e) {
+AW_DEV void c_plane_capsule(const GV& a, const GV& b, float margin, Emit& e) {
   float ax[3], p[3];
   axis_of(ax, b.mat, 2);
   for (int s = 1; s >= -1; s -= 2) {
@@ -65,7 +65,7 @@ __device__ void c_plane_capsule(const GV& a, const GV& b, float margin, Emit& e)
   }
 }
 
-__device__ void c_plane_box(const GV& a, const GV& b, float margin, Emit& e) {
+AW_DEV void c_plane_box(const GV& a, const GV& b, float margin, Emit& e) {
   float n[3], dif[3];
   axis_of(n, a.mat, 2);
   sub3(dif, b.pos, a.pos);
@@ -84,7 +84,7 @@ __device__ void c_plane_box(const GV& a, const GV& b, float margin, Emit& e) {
   }
 }
 
-__device__ void c_plane_cylinder(const GV& a, const GV& b, float margin, Emit& e) {
+AW_DEV void c_plane_cylinder(const GV& a, const GV& b, float margin, Emit& e) {
   float n[3], axis[3], dif[3], vec[3];
   axis_of(n, a.mat, 2);
   axis_of(axis, b.mat, 2);
@@ -125,7 +125,7 @@ __device__ void c_plane_cylinder(const GV& a, const GV& b, float margin, Emit& e
   }
 }
 
-__device__ void c_sphere_sphere(const float* p1, float r1, const float* p2, float r2, float margin, Emit& e) {
+AW_DEV void c_sphere_sphere(const float* p1, float r1, const float* p2, float r2, float margin, Emit& e) {
   float dif[3];
   sub3(dif, p2, p1);
   float cd = norm3(dif);
@@ -138,7 +138,7 @@ __device__ void c_sphere_sphere(const float* p1, float r1, const float* p2, floa
   emit(e, dist, pos, n);
 }
 
-__device__ void c_sphere_capsule(const GV& a, const GV& b, float margin, Emit& e) {
+AW_DEV void c_sphere_capsule(const GV& a, const GV& b, float margin, Emit& e) {
   float ax[3], dif[3], q[3];
   axis_of(ax, b.mat, 2);
   sub3(dif, a.pos, b.pos);
@@ -147,7 +147,7 @@ __device__ void c_sphere_capsule(const GV& a, const GV& b, float margin, Emit& e
   c_sphere_sphere(a.pos, a.size[0], q, b.size[0], margin, e);
 }
 
-__device__ void seg_seg(const float* p1, const float* d1, const float* p2, const float* d2, float* c1, float* c2) {
+AW_DEV void seg_seg(const float* p1, const float* d1, const float* p2, const float* d2, float* c1, float* c2) {
   float r[3];
   sub3(r, p1, p2);
   float a = dot3(d1, d1), ee = dot3(d2, d2), f = dot3(d2, r);
@@ -168,7 +168,7 @@ __device__ void seg_seg(const float* p1, const float* d1, const float* p2, const
   for (int k = 0; k < 3; k++) { c1[k] = p1[k] + d1[k] * s; c2[k] = p2[k] + d2[k] * t; }
 }
 
-__device__ void c_capsule_capsule(const GV& a, const GV& b, float margin, Emit& e) {
+AW_DEV void c_capsule_capsule(const GV& a, const GV& b, float margin, Emit& e) {
   float a1[3], a2[3], s1[3], s2[3], d1[3], d2[3], c1[3], c2[3];
   axis_of(a1, a.mat, 2);
   axis_of(a2, b.mat, 2);
@@ -180,7 +180,7 @@ __device__ void c_capsule_capsule(const GV& a, const GV& b, float margin, Emit& 
   c_sphere_sphere(c1, a.size[0], c2, b.size[0], margin, e);
 }
 
-__device__ void c_sphere_box_pt(const float* p, float r, const GV& b, float margin, Emit& e) {
+AW_DEV void c_sphere_box_pt(const float* p, float r, const GV& b, float margin, Emit& e) {
   float dif[3], loc[3], cl[3];
   sub3(dif, p, b.pos);
   mulmtv3(loc, b.mat, dif);
@@ -205,8 +205,9 @@ __device__ void c_sphere_box_pt(const float* p, float r, const GV& b, float marg
       float pk = b.size[k] - fabsf(loc[k]);
       if (pk < pen) { pen = pk; kmin = k; }
     }
-    float nl[3] = {0, 0, 0};
-    nl[kmin] = loc[kmin] >= 0 ? -1.0f : 1.0f;
+    float nl[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) nl[k] = k == kmin ? (loc[k] >= 0 ? -1.0f : 1.0f) : 0.f;
     mulmv3(n, b.mat, nl);
     dist = -pen - r;
   }
@@ -215,7 +216,7 @@ __device__ void c_sphere_box_pt(const float* p, float r, const GV& b, float marg
   emit(e, dist, pos, n);
 }
 
-__device__ float box_sdist(const float* p, const GV& b) {
+AW_DEV float box_sdist(const float* p, const GV& b) {
   float dif[3], loc[3];
   sub3(dif, p, b.pos);
   mulmtv3(loc, b.mat, dif);
@@ -229,7 +230,7 @@ __device__ float box_sdist(const float* p, const GV& b) {
   return sqrtf(out) + (mx < 0 ? mx : 0);
 }
 
-__device__ void c_capsule_box(const GV& a, const GV& b, float margin, Emit& e) {
+AW_DEV void c_capsule_box(const GV& a, const GV& b, float margin, Emit& e) {
   float ax[3], p[3];
   axis_of(ax, a.mat, 2);
   float h = a.size[1], r = a.size[0];
@@ -263,12 +264,13 @@ __device__ void c_capsule_box(const GV& a, const GV& b, float margin, Emit& e) {
   }
 }
 
-__device__ void c_box_box(const GV& A, const GV& B, float margin, Emit& e) {
+AW_DEV void c_box_box(const GV& A, const GV& B, float margin, Emit& e) {
   float a[3][3], b[3][3], t[3];
   for (int k = 0; k < 3; k++) { axis_of(a[k], A.mat, k); axis_of(b[k], B.mat, k); }
   sub3(t, B.pos, A.pos);
   float best = -1e30f, bestn[3] = {0, 0, 0};
   int bestk = -1;
+#pragma unroll
   for (int k = 0; k < 15; k++) {
     float L[3];
     if (k < 3) copy3(L, a[k]);
@@ -293,43 +295,71 @@ __device__ void c_box_box(const GV& A, const GV& B, float margin, Emit& e) {
   }
   if (bestk < 0) return;
   if (bestk < 6) {
+    // face contact; every axis / size choice is a select so all arrays stay in VGPRs
     const bool refA = bestk < 3;
-    const GV& R = refA ? A : B;
-    const GV& I = refA ? B : A;
+    const int fk = refA ? bestk : bestk - 3;
+    const int ru = fk == 2 ? 0 : fk + 1;
+    float Rpos[3], Ipos[3], Rs[3], Is[3], rN[3], rU[3], rV[3];
     float ra[3][3], ia[3][3];
+#pragma unroll
     for (int k = 0; k < 3; k++) {
-      copy3(ra[k], refA ? a[k] : b[k]);
-      copy3(ia[k], refA ? b[k] : a[k]);
+      Rpos[k] = refA ? A.pos[k] : B.pos[k];
+      Ipos[k] = refA ? B.pos[k] : A.pos[k];
+      Rs[k] = refA ? A.size[k] : B.size[k];
+      Is[k] = refA ? B.size[k] : A.size[k];
+#pragma unroll
+      for (int c = 0; c < 3; c++) { ra[k][c] = refA ? a[k][c] : b[k][c]; ia[k][c] = refA ? b[k][c] : a[k][c]; }
     }
-    int fk = refA ? bestk : bestk - 3;
+    const int rvv = (fk + 2) % 3;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      rN[c] = fk == 0 ? ra[0][c] : (fk == 1 ? ra[1][c] : ra[2][c]);
+      rU[c] = ru == 0 ? ra[0][c] : (ru == 1 ? ra[1][c] : ra[2][c]);
+      rV[c] = rvv == 0 ? ra[0][c] : (rvv == 1 ? ra[1][c] : ra[2][c]);
+    }
+    const float hF = fk == 0 ? Rs[0] : (fk == 1 ? Rs[1] : Rs[2]);
+    const float hu = ru == 0 ? Rs[0] : (ru == 1 ? Rs[1] : Rs[2]);
+    const float hv = rvv == 0 ? Rs[0] : (rvv == 1 ? Rs[1] : Rs[2]);
     float nr[3];
     copy3(nr, bestn);
     if (!refA) scl3(nr, nr, -1);
-    float sg = dot3(nr, ra[fk]) > 0 ? 1.f : -1.f;
-    int ru = (fk + 1) % 3, rv = (fk + 2) % 3;
-    float hu = R.size[ru], hv = R.size[rv];
+    const float sg = dot3(nr, rN) > 0 ? 1.f : -1.f;
     float fc[3];
-    for (int k = 0; k < 3; k++) fc[k] = R.pos[k] + ra[fk][k] * sg * R.size[fk];
+#pragma unroll
+    for (int k = 0; k < 3; k++) fc[k] = Rpos[k] + rN[k] * sg * hF;
     int ik = 0;
     float imin = 1e30f, isg = 1;
+#pragma unroll
     for (int k = 0; k < 3; k++) {
       float dd = dot3(ia[k], nr);
       if (dd < imin) { imin = dd; ik = k; isg = 1; }
       if (-dd < imin) { imin = -dd; ik = k; isg = -1; }
     }
-    int iu = (ik + 1) % 3, iv = (ik + 2) % 3;
+    const int iu = ik == 2 ? 0 : ik + 1, iv = (ik + 2) % 3;
+    float iN[3], iU[3], iV[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      iN[c] = ik == 0 ? ia[0][c] : (ik == 1 ? ia[1][c] : ia[2][c]);
+      iU[c] = iu == 0 ? ia[0][c] : (iu == 1 ? ia[1][c] : ia[2][c]);
+      iV[c] = iv == 0 ? ia[0][c] : (iv == 1 ? ia[1][c] : ia[2][c]);
+    }
+    const float sIk = ik == 0 ? Is[0] : (ik == 1 ? Is[1] : Is[2]);
+    const float su = iu == 0 ? Is[0] : (iu == 1 ? Is[1] : Is[2]);
+    const float sv = iv == 0 ? Is[0] : (iv == 1 ? Is[1] : Is[2]);
     float inn[3], ic[3];
-    scl3(inn, ia[ik], isg);
-    for (int k = 0; k < 3; k++) ic[k] = I.pos[k] + inn[k] * I.size[ik];
-    float su = I.size[iu], sv = I.size[iv];
+    scl3(inn, iN, isg);
+#pragma unroll
+    for (int k = 0; k < 3; k++) ic[k] = Ipos[k] + inn[k] * sIk;
     float P[4][3], pu[4], pv[4];
     const float cs[4][2] = {{1, 1}, {-1, 1}, {-1, -1}, {1, -1}};
+#pragma unroll
     for (int q = 0; q < 4; q++) {
-      for (int k = 0; k < 3; k++) P[q][k] = ic[k] + ia[iu][k] * cs[q][0] * su + ia[iv][k] * cs[q][1] * sv;
+#pragma unroll
+      for (int k = 0; k < 3; k++) P[q][k] = ic[k] + iU[k] * cs[q][0] * su + iV[k] * cs[q][1] * sv;
       float dv[3];
       sub3(dv, P[q], fc);
-      pu[q] = dot3(dv, ra[ru]);
-      pv[q] = dot3(dv, ra[rv]);
+      pu[q] = dot3(dv, rU);
+      pv[q] = dot3(dv, rV);
     }
     auto em = [&](const float* p) {
       float dv[3];
@@ -340,23 +370,27 @@ __device__ void c_box_box(const GV& A, const GV& B, float margin, Emit& e) {
       for (int k = 0; k < 3; k++) pos[k] = p[k] - nr[k] * dist / 2;
       emit(e, dist, pos, bestn);
     };
+#pragma unroll
     for (int q = 0; q < 4; q++)
       if (fabsf(pu[q]) <= hu && fabsf(pv[q]) <= hv) em(P[q]);
     float den = dot3(nr, inn);
     if (fabsf(den) > 1e-12f) {
+#pragma unroll
       for (int q = 0; q < 4; q++) {
         float Q[3], dq[3], Qp[3];
-        for (int k = 0; k < 3; k++) Q[k] = fc[k] + ra[ru][k] * cs[q][0] * hu + ra[rv][k] * cs[q][1] * hv;
+        for (int k = 0; k < 3; k++) Q[k] = fc[k] + rU[k] * cs[q][0] * hu + rV[k] * cs[q][1] * hv;
         sub3(dq, ic, Q);
         float tt = dot3(dq, inn) / den;
         for (int k = 0; k < 3; k++) Qp[k] = Q[k] + nr[k] * tt;
         sub3(dq, Qp, ic);
-        if (fabsf(dot3(dq, ia[iu])) <= su && fabsf(dot3(dq, ia[iv])) <= sv) em(Qp);
+        if (fabsf(dot3(dq, iU)) <= su && fabsf(dot3(dq, iV)) <= sv) em(Qp);
       }
     }
+#pragma unroll
     for (int q = 0; q < 4; q++) {
-      int q2 = (q + 1) & 3;
+      const int q2 = (q + 1) & 3;
       float du = pu[q2] - pu[q], dv = pv[q2] - pv[q];
+#pragma unroll
       for (int side = 0; side < 4; side++) {
         float tt;
         if (side < 2) {
@@ -379,24 +413,33 @@ __device__ void c_box_box(const GV& A, const GV& B, float margin, Emit& e) {
     }
     return;
   }
-  int ea = (bestk - 6) / 3, eb = (bestk - 6) % 3;
+  const int ea = (bestk - 6) / 3, eb = (bestk - 6) % 3;
   float pa[3], pb[3];
   copy3(pa, A.pos);
   copy3(pb, B.pos);
+#pragma unroll
   for (int k = 0; k < 3; k++) {
     if (k != ea) {
-      float s = dot3(a[k], bestn) > 0 ? 1.f : -1.f;
-      for (int q = 0; q < 3; q++) pa[q] += a[k][q] * s * A.size[k];
+      float s1 = dot3(a[k], bestn) > 0 ? 1.f : -1.f;
+      for (int q = 0; q < 3; q++) pa[q] += a[k][q] * s1 * A.size[k];
     }
     if (k != eb) {
-      float s = dot3(b[k], bestn) > 0 ? -1.f : 1.f;
-      for (int q = 0; q < 3; q++) pb[q] += b[k][q] * s * B.size[k];
+      float s2 = dot3(b[k], bestn) > 0 ? -1.f : 1.f;
+      for (int q = 0; q < 3; q++) pb[q] += b[k][q] * s2 * B.size[k];
     }
+  }
+  float aE[3], bE[3];
+  const float sa = ea == 0 ? A.size[0] : (ea == 1 ? A.size[1] : A.size[2]);
+  const float sb = eb == 0 ? B.size[0] : (eb == 1 ? B.size[1] : B.size[2]);
+#pragma unroll
+  for (int q = 0; q < 3; q++) {
+    aE[q] = ea == 0 ? a[0][q] : (ea == 1 ? a[1][q] : a[2][q]);
+    bE[q] = eb == 0 ? b[0][q] : (eb == 1 ? b[1][q] : b[2][q]);
   }
   float s1[3], d1[3], s2[3], d2[3], c1[3], c2[3], pos[3];
   for (int q = 0; q < 3; q++) {
-    s1[q] = pa[q] - a[ea][q] * A.size[ea]; d1[q] = 2 * a[ea][q] * A.size[ea];
-    s2[q] = pb[q] - b[eb][q] * B.size[eb]; d2[q] = 2 * b[eb][q] * B.size[eb];
+    s1[q] = pa[q] - aE[q] * sa; d1[q] = 2 * aE[q] * sa;
+    s2[q] = pb[q] - bE[q] * sb; d2[q] = 2 * bE[q] * sb;
   }
   seg_seg(s1, d1, s2, d2, c1, c2);
   for (int q = 0; q < 3; q++) pos[q] = 0.5f * (c1[q] + c2[q]);
@@ -407,23 +450,23 @@ __device__ void c_box_box(const GV& A, const GV& B, float margin, Emit& e) {
 // MPR (libccd ccdMPRPenetration), supports inflated by margin/2 (mjccd_support)
 namespace mpr {
 constexpr float EPS = 1.1920928955078125e-07f;  // FLT_EPSILON (libccd CCD_EPS for float)
-__device__ __forceinline__ bool is_zero(float x) { return fabsf(x) < EPS; }
-__device__ __forceinline__ bool eq(float a, float b) {
+AW_DEV bool is_zero(float x) { return fabsf(x) < EPS; }
+AW_DEV bool eq(float a, float b) {
   float ab = fabsf(a - b);
   if (ab < EPS) return true;
   float fa = fabsf(a), fb = fabsf(b);
   return fb > fa ? ab < EPS * fb : ab < EPS * fa;
 }
-__device__ __forceinline__ bool veq(const float* a, const float* b) { return eq(a[0], b[0]) && eq(a[1], b[1]) && eq(a[2], b[2]); }
-__device__ __forceinline__ void vnorm(float* v) {
+AW_DEV bool veq(const float* a, const float* b) { return eq(a[0], b[0]) && eq(a[1], b[1]) && eq(a[2], b[2]); }
+AW_DEV void vnorm(float* v) {
   float k = 1.0f / sqrtf(dot3(v, v));
   scl3(v, v, k);
 }
-__device__ __forceinline__ float sgn(float x) { return x < 0 ? -1.f : (x > 0 ? 1.f : 0.f); }
+AW_DEV float sgn(float x) { return x < 0 ? -1.f : (x > 0 ? 1.f : 0.f); }
 
 struct Sup { float v[3], v1[3], v2[3]; };
 
-__device__ void gsupport(float* res, const GV& g, const float* dir, float margin) {
+AW_DEV void gsupport(float* res, const GV& g, const float* dir, float margin) {
   float ld[3], r[3];
   mulmtv3(ld, g.mat, dir);
   const float* s = g.size;
@@ -443,111 +486,130 @@ __device__ void gsupport(float* res, const GV& g, const float* dir, float margin
 
 struct Ctx { const GV* g1; const GV* g2; float margin, tol; int maxit; };
 
-__device__ __forceinline__ void support(const Ctx& c, const float* dir, Sup& s) {
+AW_DEV void support(const Ctx& c, const float* dir, Sup& s) {
   float nd[3];
   scl3(nd, dir, -1);
   gsupport(s.v1, *c.g1, dir, c.margin);
   gsupport(s.v2, *c.g2, nd, c.margin);
   sub3(s.v, s.v1, s.v2);
 }
-__device__ __forceinline__ void portal_dir(const Sup* p, float* dir) {
+// the portal is kept as four named vertices (no array) so every vertex stays in VGPRs
+struct Portal { Sup p0, p1, p2, p3; };
+// element-wise copy (a whole-struct copy becomes a memcpy that keeps the portal in scratch)
+AW_DEV void setsup(Sup& d, const Sup& s) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) { d.v[k] = s.v[k]; d.v1[k] = s.v1[k]; d.v2[k] = s.v2[k]; }
+}
+
+AW_DEV void portal_dir(const Portal& P, float* dir) {
   float a[3], b[3];
-  sub3(a, p[2].v, p[1].v);
-  sub3(b, p[3].v, p[1].v);
+  sub3(a, P.p2.v, P.p1.v);
+  sub3(b, P.p3.v, P.p1.v);
   cross3(dir, a, b);
   vnorm(dir);
 }
-__device__ __forceinline__ bool reach_tol(const Sup* p, const Sup& v4, const float* dir, float tol) {
-  float dv1 = dot3(p[1].v, dir), dv2 = dot3(p[2].v, dir), dv3 = dot3(p[3].v, dir), dv4 = dot3(v4.v, dir);
+AW_DEV bool reach_tol(const Portal& P, const Sup& v4, const float* dir, float tol) {
+  float dv1 = dot3(P.p1.v, dir), dv2 = dot3(P.p2.v, dir), dv3 = dot3(P.p3.v, dir), dv4 = dot3(v4.v, dir);
   float d1 = fminf(fminf(dv4 - dv1, dv4 - dv2), dv4 - dv3);
   return eq(d1, tol) || d1 < tol;
 }
-__device__ __forceinline__ void expand(Sup* p, const Sup& v4) {
-  float v4v0[3];
-  cross3(v4v0, v4.v, p[0].v);
-  float d = dot3(p[1].v, v4v0);
-  if (d > 0) {
-    d = dot3(p[2].v, v4v0);
-    if (d > 0) p[1] = v4; else p[3] = v4;
-  } else {
-    d = dot3(p[3].v, v4v0);
-    if (d > 0) p[2] = v4; else p[1] = v4;
+AW_DEV void selsup(Sup& d, bool c, const Sup& s) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    d.v[k] = c ? s.v[k] : d.v[k]; d.v1[k] = c ? s.v1[k] : d.v1[k]; d.v2[k] = c ? s.v2[k] : d.v2[k];
   }
 }
-__device__ int discover(const Ctx& c, Sup* p) {
+// branch-free vertex replacement: conditional struct stores through a selected pointer would
+// pin the portal in scratch
+AW_DEV void expand(Portal& P, const Sup& v4) {
+  float v4v0[3];
+  cross3(v4v0, v4.v, P.p0.v);
+  const bool a1 = dot3(P.p1.v, v4v0) > 0;
+  const bool a2 = dot3(P.p2.v, v4v0) > 0;
+  const bool a3 = dot3(P.p3.v, v4v0) > 0;
+  selsup(P.p1, (a1 && a2) || (!a1 && !a3), v4);
+  selsup(P.p3, a1 && !a2, v4);
+  selsup(P.p2, !a1 && a3, v4);
+}
+AW_DEV int discover(const Ctx& c, Portal& P) {
   float dir[3], va[3], vb[3];
-  copy3(p[0].v1, c.g1->pos);
-  copy3(p[0].v2, c.g2->pos);
-  sub3(p[0].v, p[0].v1, p[0].v2);
+  copy3(P.p0.v1, c.g1->pos);
+  copy3(P.p0.v2, c.g2->pos);
+  sub3(P.p0.v, P.p0.v1, P.p0.v2);
   const float zero[3] = {0, 0, 0};
-  if (veq(p[0].v, zero)) p[0].v[0] += EPS * 10;
-  scl3(dir, p[0].v, -1);
+  if (veq(P.p0.v, zero)) P.p0.v[0] += EPS * 10;
+  scl3(dir, P.p0.v, -1);
   vnorm(dir);
-  support(c, dir, p[1]);
-  float d = dot3(p[1].v, dir);
+  support(c, dir, P.p1);
+  float d = dot3(P.p1.v, dir);
   if (is_zero(d) || d < 0) return -1;
-  cross3(dir, p[0].v, p[1].v);
-  if (is_zero(dot3(dir, dir))) return veq(p[1].v, zero) ? 1 : 2;
+  cross3(dir, P.p0.v, P.p1.v);
+  if (is_zero(dot3(dir, dir))) return veq(P.p1.v, zero) ? 1 : 2;
   vnorm(dir);
-  support(c, dir, p[2]);
-  d = dot3(p[2].v, dir);
+  support(c, dir, P.p2);
+  d = dot3(P.p2.v, dir);
   if (is_zero(d) || d < 0) return -1;
-  sub3(va, p[1].v, p[0].v);
-  sub3(vb, p[2].v, p[0].v);
+  sub3(va, P.p1.v, P.p0.v);
+  sub3(vb, P.p2.v, P.p0.v);
   cross3(dir, va, vb);
   vnorm(dir);
-  if (dot3(dir, p[0].v) > 0) {
-    Sup t = p[1]; p[1] = p[2]; p[2] = t;
-    scl3(dir, dir, -1);
+  {
+    const bool sw = dot3(dir, P.p0.v) > 0;
+    Sup t;
+    setsup(t, P.p1);
+    selsup(P.p1, sw, P.p2);
+    selsup(P.p2, sw, t);
+    if (sw) scl3(dir, dir, -1);
   }
   for (int it = 0; it < 1000; it++) {
-    support(c, dir, p[3]);
-    d = dot3(p[3].v, dir);
+    support(c, dir, P.p3);
+    d = dot3(P.p3.v, dir);
     if (is_zero(d) || d < 0) return -1;
-    bool cont = false;
-    cross3(va, p[1].v, p[3].v);
-    d = dot3(va, p[0].v);
-    if (d < 0 && !is_zero(d)) { p[2] = p[3]; cont = true; }
-    if (!cont) {
-      cross3(va, p[3].v, p[2].v);
-      d = dot3(va, p[0].v);
-      if (d < 0 && !is_zero(d)) { p[1] = p[3]; cont = true; }
-    }
-    if (!cont) return 0;
-    sub3(va, p[1].v, p[0].v);
-    sub3(vb, p[2].v, p[0].v);
+    cross3(va, P.p1.v, P.p3.v);
+    d = dot3(va, P.p0.v);
+    const bool r2 = d < 0 && !is_zero(d);
+    cross3(va, P.p3.v, P.p2.v);
+    d = dot3(va, P.p0.v);
+    const bool r1 = !r2 && d < 0 && !is_zero(d);
+    if (!r2 && !r1) return 0;
+    selsup(P.p2, r2, P.p3);
+    selsup(P.p1, r1, P.p3);
+    sub3(va, P.p1.v, P.p0.v);
+    sub3(vb, P.p2.v, P.p0.v);
     cross3(dir, va, vb);
     vnorm(dir);
   }
   return -1;
 }
-__device__ int refine(const Ctx& c, Sup* p) {
+AW_DEV int refine(const Ctx& c, Portal& P) {
   float dir[3];
   Sup v4;
   for (int it = 0; it <= c.maxit; it++) {
-    portal_dir(p, dir);
-    float d = dot3(dir, p[1].v);
+    portal_dir(P, dir);
+    float d = dot3(dir, P.p1.v);
     if (is_zero(d) || d > 0) return 0;
     support(c, dir, v4);
     float d4 = dot3(v4.v, dir);
-    if (!(is_zero(d4) || d4 > 0) || reach_tol(p, v4, dir, c.tol)) return -1;
-    expand(p, v4);
+    if (!(is_zero(d4) || d4 > 0) || reach_tol(P, v4, dir, c.tol)) return -1;
+    expand(P, v4);
   }
   return -1;
 }
-__device__ float pseg2(const float* P, const float* x0, const float* b, float* w) {
+AW_DEV float pseg2(const float* P, const float* x0, const float* b, float* w) {
   float dd[3], a[3];
   sub3(dd, b, x0);
   sub3(a, x0, P);
   float t = -dot3(a, dd) / dot3(dd, dd);
-  if (t < 0 || is_zero(t)) copy3(w, x0);
-  else if (t > 1 || eq(t, 1)) copy3(w, b);
-  else for (int k = 0; k < 3; k++) w[k] = x0[k] + dd[k] * t;
+  const bool lo = t < 0 || is_zero(t), hi = !lo && (t > 1 || eq(t, 1));
   float df[3];
-  sub3(df, w, P);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    w[k] = lo ? x0[k] : (hi ? b[k] : x0[k] + dd[k] * t);
+    df[k] = w[k] - P[k];
+  }
   return dot3(df, df);
 }
-__device__ float ptri2(const float* P, const float* x0, const float* B, const float* C, float* w) {
+AW_DEV float ptri2(const float* P, const float* x0, const float* B, const float* C, float* w) {
   float d1[3], d2[3], a[3];
   sub3(d1, B, x0);
   sub3(d2, C, x0);
@@ -566,68 +628,77 @@ __device__ float ptri2(const float* P, const float* x0, const float* B, const fl
   float w2[3];
   float dist = pseg2(P, x0, B, w);
   float d2s = pseg2(P, x0, C, w2);
-  if (d2s < dist) { dist = d2s; copy3(w, w2); }
+  bool take = d2s < dist;
+  dist = take ? d2s : dist;
+#pragma unroll
+  for (int k = 0; k < 3; k++) w[k] = take ? w2[k] : w[k];
   d2s = pseg2(P, B, C, w2);
-  if (d2s < dist) { dist = d2s; copy3(w, w2); }
+  take = d2s < dist;
+  dist = take ? d2s : dist;
+#pragma unroll
+  for (int k = 0; k < 3; k++) w[k] = take ? w2[k] : w[k];
   return dist;
 }
-__device__ void find_pos(const Sup* p, float* pos) {
-  float dir[3], vec[3], b[4];
-  portal_dir(p, dir);
-  cross3(vec, p[1].v, p[2].v); b[0] = dot3(vec, p[3].v);
-  cross3(vec, p[3].v, p[2].v); b[1] = dot3(vec, p[0].v);
-  cross3(vec, p[0].v, p[1].v); b[2] = dot3(vec, p[3].v);
-  cross3(vec, p[2].v, p[1].v); b[3] = dot3(vec, p[0].v);
-  float sum = b[0] + b[1] + b[2] + b[3];
+AW_DEV void find_pos(const Portal& P, float* pos) {
+  float dir[3], vec[3], b0, b1, b2, b3;
+  portal_dir(P, dir);
+  cross3(vec, P.p1.v, P.p2.v); b0 = dot3(vec, P.p3.v);
+  cross3(vec, P.p3.v, P.p2.v); b1 = dot3(vec, P.p0.v);
+  cross3(vec, P.p0.v, P.p1.v); b2 = dot3(vec, P.p3.v);
+  cross3(vec, P.p2.v, P.p1.v); b3 = dot3(vec, P.p0.v);
+  float sum = b0 + b1 + b2 + b3;
   if (is_zero(sum) || sum < 0) {
-    b[0] = 0;
-    cross3(vec, p[2].v, p[3].v); b[1] = dot3(vec, dir);
-    cross3(vec, p[3].v, p[1].v); b[2] = dot3(vec, dir);
-    cross3(vec, p[1].v, p[2].v); b[3] = dot3(vec, dir);
-    sum = b[1] + b[2] + b[3];
+    b0 = 0;
+    cross3(vec, P.p2.v, P.p3.v); b1 = dot3(vec, dir);
+    cross3(vec, P.p3.v, P.p1.v); b2 = dot3(vec, dir);
+    cross3(vec, P.p1.v, P.p2.v); b3 = dot3(vec, dir);
+    sum = b1 + b2 + b3;
   }
-  float inv = 1.0f / sum, p1[3] = {0, 0, 0}, p2[3] = {0, 0, 0};
-  for (int i = 0; i < 4; i++)
-    for (int k = 0; k < 3; k++) { p1[k] += p[i].v1[k] * b[i]; p2[k] += p[i].v2[k] * b[i]; }
-  for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p1[k] + p2[k]) * inv;
+  float inv = 1.0f / sum;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    float p1 = P.p0.v1[k] * b0 + P.p1.v1[k] * b1 + P.p2.v1[k] * b2 + P.p3.v1[k] * b3;
+    float p2 = P.p0.v2[k] * b0 + P.p1.v2[k] * b1 + P.p2.v2[k] * b2 + P.p3.v2[k] * b3;
+    pos[k] = 0.5f * (p1 + p2) * inv;
+  }
 }
-__device__ int penetration(const Ctx& c, float* depth, float* dir, float* pos) {
-  Sup p[4];
-  int res = discover(c, p);
+AW_DEV int penetration(const Ctx& c, float* depth, float* dir, float* pos) {
+  Portal P;
+  int res = discover(c, P);
   if (res < 0) return -1;
   if (res == 1) {
     *depth = 0;
     dir[0] = dir[1] = dir[2] = 0;
-    for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p[1].v1[k] + p[1].v2[k]);
+    for (int k = 0; k < 3; k++) pos[k] = 0.5f * (P.p1.v1[k] + P.p1.v2[k]);
     return 0;
   }
   if (res == 2) {
-    for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p[1].v1[k] + p[1].v2[k]);
-    copy3(dir, p[1].v);
+    for (int k = 0; k < 3; k++) pos[k] = 0.5f * (P.p1.v1[k] + P.p1.v2[k]);
+    copy3(dir, P.p1.v);
     *depth = sqrtf(dot3(dir, dir));
     vnorm(dir);
     return 0;
   }
-  if (refine(c, p) < 0) return -1;
+  if (refine(c, P) < 0) return -1;
   Sup v4;
   float pd[3];
   for (int it = 0;; it++) {
-    portal_dir(p, pd);
+    portal_dir(P, pd);
     support(c, pd, v4);
-    if (reach_tol(p, v4, pd, c.tol) || it > c.maxit) {
+    if (reach_tol(P, v4, pd, c.tol) || it > c.maxit) {
       const float zero[3] = {0, 0, 0};
-      *depth = sqrtf(ptri2(zero, p[1].v, p[2].v, p[3].v, dir));
+      *depth = sqrtf(ptri2(zero, P.p1.v, P.p2.v, P.p3.v, dir));
       if (is_zero(*depth)) dir[0] = dir[1] = dir[2] = 0;
       else vnorm(dir);
-      find_pos(p, pos);
+      find_pos(P, pos);
       return 0;
     }
-    expand(p, v4);
+    expand(P, v4);
   }
 }
 }  // namespace mpr
 
-__device__ void c_convex(const DModel& m, const GV& a, const GV& b, float margin, Emit& e) {
+AW_DEV void c_convex(const DModel& m, const GV& a, const GV& b, float margin, Emit& e) {
   mpr::Ctx ctx{&a, &b, margin, m.mpr_tolerance, m.mpr_iterations};
   float depth, dir[3], pos[3];
   if (mpr::penetration(ctx, &depth, dir, pos) != 0) return;
@@ -638,7 +709,7 @@ __device__ void c_convex(const DModel& m, const GV& a, const GV& b, float margin
 }
 
 // ---------------------------------------------------------------------------------------
-__device__ void collide_pair(const DModel& m, Env& s, int pair) {
+AW_DEV void collide_pair(const DModel& m, Env& s, int pair) {
   int g1 = m.cp_g1[pair], g2 = m.cp_g2[pair];
   GV a, b;
   a.type = m.geom_type[g1];
@@ -655,6 +726,11 @@ __device__ void collide_pair(const DModel& m, Env& s, int pair) {
   }
   for (int k = 0; k < 9; k++) { a.mat[k] = s.gxmat[g1][k]; b.mat[k] = s.gxmat[g2][k]; }
   Emit e{&s, pair, 0};
+  // every non-plane pair with a cylinder goes through MPR (mjc_Convex); one inlined call site
+  if (a.type != GEOM_PLANE && (a.type == GEOM_CYLINDER || b.type == GEOM_CYLINDER)) {
+    c_convex(m, a, b, margin, e);
+    return;
+  }
   switch (a.type) {
     case GEOM_PLANE:
       if (b.type == GEOM_SPHERE) c_plane_sphere(a.pos, a.mat, b.pos, b.size[0], margin, e);
@@ -665,16 +741,11 @@ __device__ void collide_pair(const DModel& m, Env& s, int pair) {
     case GEOM_SPHERE:
       if (b.type == GEOM_SPHERE) c_sphere_sphere(a.pos, a.size[0], b.pos, b.size[0], margin, e);
       else if (b.type == GEOM_CAPSULE) c_sphere_capsule(a, b, margin, e);
-      else if (b.type == GEOM_CYLINDER) c_convex(m, a, b, margin, e);
       else if (b.type == GEOM_BOX) c_sphere_box_pt(a.pos, a.size[0], b, margin, e);
       break;
     case GEOM_CAPSULE:
       if (b.type == GEOM_CAPSULE) c_capsule_capsule(a, b, margin, e);
-      else if (b.type == GEOM_CYLINDER) c_convex(m, a, b, margin, e);
       else if (b.type == GEOM_BOX) c_capsule_box(a, b, margin, e);
-      break;
-    case GEOM_CYLINDER:
-      c_convex(m, a, b, margin, e);
       break;
     case GEOM_BOX:
       if (b.type == GEOM_BOX) c_box_box(a, b, margin, e);

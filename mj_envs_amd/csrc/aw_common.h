@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#define AW_DEV __device__ __attribute__((always_inline)) inline
+
 namespace aw {
 
 constexpr int MAXV = 36;      // dofs (relocate: 36)
@@ -106,19 +108,27 @@ struct __attribute__((aligned(16))) Env {
   float bpos[MAXB][3], bquat[MAXB][4], bmass[MAXB];
   float spos[MAXS][3];
   float gpos[MAXG][3], gsize[MAXG][3];
-  // position stage
-  float xpos[MAXB][3], xquat[MAXB][4], xmat[MAXB][9], xipos[MAXB][3], subcom[MAXB][3];
-  float cinert[MAXB][10];
+  // position stage (kept through the step: obs/reward read these after the last substep)
+  float xpos[MAXB][3], xquat[MAXB][4], xmat[MAXB][9];
+  // stage arrays that are dead once the constraint rows exist; their storage is reused by
+  // the noslip pass for X = inv(M) J_edges'
   union {
-    struct { float crb[MAXB][10]; float buf[MAXV][6]; } p;     // M build
-    struct { float cvel[MAXB][6]; float cacc[MAXB][6]; } v;    // velocity stage (cacc -> cfrc)
-  } u1;
-  union {
-    struct { float xaxis[MAXV][3]; float xanchor[MAXV][3]; } j;
-    float cdof_dot[MAXV][6];
-  } u2;
-  float cdof[MAXV][6];
-  float gxpos[MAXG][3], gxmat[MAXG][9];
+    struct {
+      float xipos[MAXB][3], subcom[MAXB][3];
+      float cinert[MAXB][10];
+      union {
+        struct { float crb[MAXB][10]; float buf[MAXV][6]; } p;     // M build
+        struct { float cvel[MAXB][6]; float cacc[MAXB][6]; } v;    // velocity stage (cacc -> cfrc)
+      } u1;
+      union {
+        struct { float xaxis[MAXV][3]; float xanchor[MAXV][3]; } j;
+        float cdof_dot[MAXV][6];
+      } u2;
+      float cdof[MAXV][6];
+      float gxpos[MAXG][3], gxmat[MAXG][9];
+    };
+    float X[MAXDENSE][VS];
+  };
   float sxpos[MAXS][3];
   float txmat[MAXTOUCH][9];
   float tlen[MAXT];
@@ -145,24 +155,24 @@ struct __attribute__((aligned(16))) Env {
 
 // ---------------------------------------------------------------------------------------
 // wave primitives
-__device__ __forceinline__ float rlane(float x, int l) {
+AW_DEV float rlane(float x, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
 }
-__device__ __forceinline__ int rlane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
-__device__ __forceinline__ void wsync() { __syncthreads(); }
+AW_DEV int rlane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+AW_DEV void wsync() { __syncthreads(); }
 
-__device__ __forceinline__ float wave_sum(float x) {
+AW_DEV float wave_sum(float x) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
   return x;
 }
-__device__ __forceinline__ float wave_max(float x) {
+AW_DEV float wave_max(float x) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
   return x;
 }
 // exclusive prefix sum of small non-negative ints across the wave
-__device__ __forceinline__ int wave_excl_scan(int x, int lane, int* total) {
+AW_DEV int wave_excl_scan(int x, int lane, int* total) {
   int v = x;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -175,43 +185,43 @@ __device__ __forceinline__ int wave_excl_scan(int x, int lane, int* total) {
 
 // ---------------------------------------------------------------------------------------
 // fp32 3D helpers
-__device__ __forceinline__ float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-__device__ __forceinline__ void cross3(float* r, const float* a, const float* b) {
+AW_DEV float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+AW_DEV void cross3(float* r, const float* a, const float* b) {
   float t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
   r[0] = t0; r[1] = t1; r[2] = t2;
 }
-__device__ __forceinline__ void sub3(float* r, const float* a, const float* b) { r[0] = a[0] - b[0]; r[1] = a[1] - b[1]; r[2] = a[2] - b[2]; }
-__device__ __forceinline__ void add3(float* r, const float* a, const float* b) { r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2]; }
-__device__ __forceinline__ void scl3(float* r, const float* a, float s) { r[0] = a[0] * s; r[1] = a[1] * s; r[2] = a[2] * s; }
-__device__ __forceinline__ void copy3(float* r, const float* a) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; }
-__device__ __forceinline__ float norm3(const float* a) { return sqrtf(dot3(a, a)); }
-__device__ __forceinline__ float normalize3(float* a) {
+AW_DEV void sub3(float* r, const float* a, const float* b) { r[0] = a[0] - b[0]; r[1] = a[1] - b[1]; r[2] = a[2] - b[2]; }
+AW_DEV void add3(float* r, const float* a, const float* b) { r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2]; }
+AW_DEV void scl3(float* r, const float* a, float s) { r[0] = a[0] * s; r[1] = a[1] * s; r[2] = a[2] * s; }
+AW_DEV void copy3(float* r, const float* a) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; }
+AW_DEV float norm3(const float* a) { return sqrtf(dot3(a, a)); }
+AW_DEV float normalize3(float* a) {
   float n = norm3(a);
   if (n < MINVAL) { a[0] = 1; a[1] = 0; a[2] = 0; return n; }
   float in = 1.0f / n;
   a[0] *= in; a[1] *= in; a[2] *= in;
   return n;
 }
-__device__ __forceinline__ void mulmv3(float* r, const float* m, const float* v) {
+AW_DEV void mulmv3(float* r, const float* m, const float* v) {
   float t0 = m[0] * v[0] + m[1] * v[1] + m[2] * v[2];
   float t1 = m[3] * v[0] + m[4] * v[1] + m[5] * v[2];
   float t2 = m[6] * v[0] + m[7] * v[1] + m[8] * v[2];
   r[0] = t0; r[1] = t1; r[2] = t2;
 }
-__device__ __forceinline__ void mulmtv3(float* r, const float* m, const float* v) {
+AW_DEV void mulmtv3(float* r, const float* m, const float* v) {
   float t0 = m[0] * v[0] + m[3] * v[1] + m[6] * v[2];
   float t1 = m[1] * v[0] + m[4] * v[1] + m[7] * v[2];
   float t2 = m[2] * v[0] + m[5] * v[1] + m[8] * v[2];
   r[0] = t0; r[1] = t1; r[2] = t2;
 }
-__device__ __forceinline__ void mulq(float* r, const float* a, const float* b) {
+AW_DEV void mulq(float* r, const float* a, const float* b) {
   float t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
   float t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
   float t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
   float t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
   r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
 }
-__device__ __forceinline__ void rotvq(float* r, const float* v, const float* q) {
+AW_DEV void rotvq(float* r, const float* v, const float* q) {
   float u[3] = {q[1], q[2], q[3]}, t[3], t2[3];
   cross3(t, u, v);
   scl3(t, t, 2.0f);
@@ -220,22 +230,22 @@ __device__ __forceinline__ void rotvq(float* r, const float* v, const float* q) 
   r[1] = v[1] + q[0] * t[1] + t2[1];
   r[2] = v[2] + q[0] * t[2] + t2[2];
 }
-__device__ __forceinline__ void q2m(float* m, const float* q) {
+AW_DEV void q2m(float* m, const float* q) {
   float w = q[0], x = q[1], y = q[2], z = q[3];
   m[0] = 1 - 2 * (y * y + z * z); m[1] = 2 * (x * y - w * z); m[2] = 2 * (x * z + w * y);
   m[3] = 2 * (x * y + w * z); m[4] = 1 - 2 * (x * x + z * z); m[5] = 2 * (y * z - w * x);
   m[6] = 2 * (x * z - w * y); m[7] = 2 * (y * z + w * x); m[8] = 1 - 2 * (x * x + y * y);
 }
-__device__ __forceinline__ void normq(float* q) {
+AW_DEV void normq(float* q) {
   float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
   if (n < MINVAL) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
   float in = 1.0f / n;
   q[0] *= in; q[1] *= in; q[2] *= in; q[3] *= in;
 }
-__device__ __forceinline__ float clampf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+AW_DEV float clampf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
 // mju_makeFrame
-__device__ __forceinline__ void make_frame(float* f) {
+AW_DEV void make_frame(float* f) {
   normalize3(f);
   if (norm3(f + 3) < 0.5f) {
     if (fabsf(f[1]) < 0.5f) { f[3] = 0; f[4] = 1; f[5] = 0; }
@@ -248,7 +258,7 @@ __device__ __forceinline__ void make_frame(float* f) {
 }
 
 // spatial algebra, MuJoCo layout (motion = [ang; lin]; cinert = [Ixx Iyy Izz Ixy Ixz Iyz mc m])
-__device__ __forceinline__ void mul_inert_vec(float* r, const float* i, const float* v) {
+AW_DEV void mul_inert_vec(float* r, const float* i, const float* v) {
   r[0] = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
   r[1] = i[3] * v[0] + i[1] * v[1] + i[5] * v[2] + i[8] * v[3] - i[6] * v[5];
   r[2] = i[4] * v[0] + i[5] * v[1] + i[2] * v[2] - i[7] * v[3] + i[6] * v[4];
@@ -256,7 +266,7 @@ __device__ __forceinline__ void mul_inert_vec(float* r, const float* i, const fl
   r[4] = i[6] * v[2] - i[8] * v[0] + i[9] * v[4];
   r[5] = i[7] * v[0] - i[6] * v[1] + i[9] * v[5];
 }
-__device__ __forceinline__ void cross_motion(float* r, const float* v, const float* u) {
+AW_DEV void cross_motion(float* r, const float* v, const float* u) {
   float t[6];
   t[0] = -v[2] * u[1] + v[1] * u[2];
   t[1] = v[2] * u[0] - v[0] * u[2];
@@ -267,7 +277,7 @@ __device__ __forceinline__ void cross_motion(float* r, const float* v, const flo
 #pragma unroll
   for (int k = 0; k < 6; k++) r[k] = t[k];
 }
-__device__ __forceinline__ void cross_force(float* r, const float* v, const float* f) {
+AW_DEV void cross_force(float* r, const float* v, const float* f) {
   float t[6];
   t[0] = -v[2] * f[1] + v[1] * f[2] - v[5] * f[4] + v[4] * f[5];
   t[1] = v[2] * f[0] - v[0] * f[2] + v[5] * f[3] - v[3] * f[5];
@@ -278,7 +288,7 @@ __device__ __forceinline__ void cross_force(float* r, const float* v, const floa
 #pragma unroll
   for (int k = 0; k < 6; k++) r[k] = t[k];
 }
-__device__ __forceinline__ float dot6(const float* a, const float* b) {
+AW_DEV float dot6(const float* a, const float* b) {
   return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
 }
 

@@ -11,7 +11,7 @@ namespace aw {
 
 // ---------------------------------------------------------------------------------------
 // stage the per-env model copies (body_pos/quat/mass, site_pos, geom_pos/size) + overrides
-__device__ void stage_model(const DModel& m, Env& s, const float* params, int lane) {
+AW_DEV void stage_model(const DModel& m, Env& s, const float* params, int lane) {
   for (int b = lane; b < m.nbody; b += 64) {
     for (int k = 0; k < 3; k++) s.bpos[b][k] = m.body_pos[3 * b + k];
     for (int k = 0; k < 4; k++) s.bquat[b][k] = m.body_quat[4 * b + k];
@@ -40,7 +40,7 @@ __device__ void stage_model(const DModel& m, Env& s, const float* params, int la
 }
 
 // mj_kinematics (+ local2global for geoms, sites)
-__device__ void stage_kinematics(const DModel& m, Env& s, int lane) {
+AW_DEV void stage_kinematics(const DModel& m, Env& s, int lane) {
   if (lane == 0) {
     s.xpos[0][0] = s.xpos[0][1] = s.xpos[0][2] = 0;
     s.xquat[0][0] = 1; s.xquat[0][1] = s.xquat[0][2] = s.xquat[0][3] = 0;
@@ -118,7 +118,7 @@ __device__ void stage_kinematics(const DModel& m, Env& s, int lane) {
 }
 
 // mj_comPos: subtree com (divided by the compile-time subtree mass), cinert, cdof
-__device__ void stage_com(const DModel& m, Env& s, int lane) {
+AW_DEV void stage_com(const DModel& m, Env& s, int lane) {
   for (int b = lane; b < m.nbody; b += 64) {
     float acc[3] = {0, 0, 0};
     for (int d = b; d < m.body_subtree_end[b]; d++) {
@@ -177,7 +177,7 @@ __device__ void stage_com(const DModel& m, Env& s, int lane) {
 // mj_crb -> M row per lane (registers).  M[i][k] = cdof_k . (crb_{body i} cdof_i) for k an
 // ancestor of i, symmetric for descendants, + armature on the diagonal.
 template <int NV>
-__device__ void stage_crb(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
+AW_DEV void stage_crb(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
   for (int b = lane; b < m.nbody; b += 64) {
     float acc[10];
     for (int k = 0; k < 10; k++) acc[k] = 0;
@@ -211,7 +211,7 @@ __device__ void stage_crb(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) 
 }
 
 // mj_comVel + mj_rne(flg_acc=0) + mj_passive + mj_fwdActuation -> qfrc_smooth
-__device__ void stage_velocity(const DModel& m, Env& s, int lane) {
+AW_DEV void stage_velocity(const DModel& m, Env& s, int lane) {
   float (*cvel)[6] = s.u1.v.cvel;
   float (*cacc)[6] = s.u1.v.cacc;
   if (lane == 0) {

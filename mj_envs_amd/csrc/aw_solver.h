@@ -19,7 +19,7 @@ namespace aw {
 // ---------------------------------------------------------------------------------------
 // dense Cholesky of a lane-distributed SPD matrix (lane i holds row i; lower part used)
 template <int NV>
-__device__ __forceinline__ void chol_factor(float (&row)[NV], int lane, float& invd) {
+AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd) {
 #pragma unroll
   for (int j = 0; j < NV; j++) {
     float djj = rlane(row[j], j);
@@ -35,7 +35,7 @@ __device__ __forceinline__ void chol_factor(float (&row)[NV], int lane, float& i
   }
 }
 template <int NV>
-__device__ __forceinline__ void chol_store(const float (&row)[NV], int lane, Env& s) {
+AW_DEV void chol_store(const float (&row)[NV], int lane, Env& s) {
   if (lane < NV) {
 #pragma unroll
     for (int k = 0; k < NV; k++)
@@ -44,7 +44,7 @@ __device__ __forceinline__ void chol_store(const float (&row)[NV], int lane, Env
 }
 // x = inv(L L') b, b lane-distributed; L rows in registers (forward) and in LDS (backward)
 template <int NV>
-__device__ __forceinline__ float chol_solve(const float (&row)[NV], float invd, float b, int lane, const Env& s) {
+AW_DEV float chol_solve(const float (&row)[NV], float invd, float b, int lane, const Env& s) {
 #pragma unroll
   for (int j = 0; j < NV; j++) {
     float yj = rlane(b, j) * rlane(invd, j);
@@ -61,7 +61,7 @@ __device__ __forceinline__ float chol_solve(const float (&row)[NV], float invd, 
 }
 // y = M x with M lane-distributed rows and x lane-distributed
 template <int NV>
-__device__ __forceinline__ float matvec(const float (&row)[NV], float x) {
+AW_DEV float matvec(const float (&row)[NV], float x) {
   float acc = 0.f;
 #pragma unroll
   for (int k = 0; k < NV; k++) acc = fmaf(row[k], rlane(x, k), acc);
@@ -69,7 +69,7 @@ __device__ __forceinline__ float matvec(const float (&row)[NV], float x) {
 }
 
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ float getimpedance(const float* solimp, float pm) {
+AW_DEV float getimpedance(const float* solimp, float pm) {
   float d0 = clampf(solimp[0], 0.0001f, 0.9999f), dmax = clampf(solimp[1], 0.0001f, 0.9999f);
   if (d0 == dmax || solimp[2] <= MINVAL) return 0.5f * (d0 + dmax);
   float x = fabsf(pm / solimp[2]);
@@ -83,7 +83,7 @@ __device__ __forceinline__ float getimpedance(const float* solimp, float pm) {
 
 // J_r . x  (x in LDS)
 template <int NV>
-__device__ __forceinline__ float row_dot(const Env& s, int r, const float* x) {
+AW_DEV float row_dot(const Env& s, int r, const float* x) {
   if (r < s.nsparse) {
     int i1 = s.efc_i1[r];
     return s.efc_v0[r] * x[s.efc_i0[r]] + (i1 >= 0 ? s.efc_v1[r] * x[i1] : 0.f);
@@ -97,7 +97,7 @@ __device__ __forceinline__ float row_dot(const Env& s, int r, const float* x) {
 
 // out_k = (J' f)_k for k = lane; f given per row in s.rowbuf (must be written + synced)
 template <int NV>
-__device__ float jt_mul(Env& s, int lane) {
+AW_DEV float jt_mul(Env& s, int lane) {
   if (lane < NV) s.vec2[lane] = 0.f;
   wsync();
   for (int r = lane; r < s.nsparse; r += 64) {
@@ -118,7 +118,7 @@ __device__ float jt_mul(Env& s, int lane) {
 // ---------------------------------------------------------------------------------------
 // mj_makeConstraint + mj_makeImpedance + reference acceleration
 template <int NV>
-__device__ void stage_constraints(const DModel& m, Env& s, int lane) {
+AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
   if (m.disableflags & DSBL_CONSTRAINT) {
     if (lane == 0) { s.nefc = s.nsparse = s.ndense = 0; }
     wsync();
@@ -299,7 +299,7 @@ struct RowR {
   int st, fr, valid;
 };
 
-__device__ __forceinline__ float row_eval(const RowR& r, float jar, float* force, int* st) {
+AW_DEV float row_eval(const RowR& r, float jar, float* force, int* st) {
   if (!r.valid) { *force = 0.f; *st = S_SAT; return 0.f; }
   if (r.fr) {
     float f = r.floss, R = 1.f / r.D;
@@ -312,7 +312,7 @@ __device__ __forceinline__ float row_eval(const RowR& r, float jar, float* force
 }
 
 template <int NV>
-__device__ void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[NV], float& a) {
+AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[NV], float& a) {
   const int nefc = s.nefc;
   const float fs = lane < NV ? s.qfrc_smooth[lane] : 0.f;
   const float a0 = lane < NV ? s.qacc_smooth[lane] : 0.f;
@@ -463,24 +463,28 @@ __device__ void solve_newton(const DModel& m, Env& s, int lane, const float (&Mr
 // ---------------------------------------------------------------------------------------
 // noslip: PGS over frictionloss rows and opposing pyramid-edge pairs, no regularisation
 template <int NV>
-__device__ void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[NV], float& qacc) {
+AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[NV], float& qacc) {
   const int nsparse = s.nsparse, ndense = s.ndense;
-  // inv(M): factor, then lane i solves M x = e_i (multi-RHS, L entries broadcast from LDS)
-  float row[NV];
-#pragma unroll
-  for (int k = 0; k < NV; k++) row[k] = Mrow[k];
-  float invd = 1.f;
-  chol_factor<NV>(row, lane, invd);
-  chol_store<NV>(row, lane, s);
-  if (lane < NV) s.vec2[lane] = invd;
-  wsync();
+  // inv(M): factor, then lane i solves M x = e_i (multi-RHS, L entries broadcast from LDS);
+  // lane i keeps row i of inv(M) in VGPRs (symmetric: row == column)
   float Mi[NV];
+  {
+    float row[NV];
+#pragma unroll
+    for (int k = 0; k < NV; k++) row[k] = Mrow[k];
+    float invd = 1.f;
+    chol_factor<NV>(row, lane, invd);
+    chol_store<NV>(row, lane, s);
+    if (lane < NV) s.vec2[lane] = invd;
+    wsync();
+  }
 #pragma unroll
   for (int j = 0; j < NV; j++) {
     float acc = (j == lane) ? 1.f : 0.f;
 #pragma unroll
     for (int k = 0; k < j; k++) acc = fmaf(-s.L[j][k], Mi[k], acc);
     Mi[j] = acc * s.vec2[j];
+    __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
   for (int j = NV - 1; j >= 0; j--) {
@@ -488,32 +492,31 @@ __device__ void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mr
 #pragma unroll
     for (int k = j + 1; k < NV; k++) acc = fmaf(-s.L[k][j], Mi[k], acc);
     Mi[j] = acc * s.vec2[j];
+    __builtin_amdgcn_sched_barrier(0);
   }
   if (lane >= NV) {
 #pragma unroll
     for (int k = 0; k < NV; k++) Mi[k] = 0.f;
   }
-  // X[e] = (inv(M) J_e')_lane for pyramidal dense rows
-  float X[MAXDENSE];
-#pragma unroll
-  for (int e = 0; e < MAXDENSE; e++) {
-    float acc = 0.f;
-    if (e < ndense && s.efc_type[nsparse + e] == C_CON_PYRAMIDAL) {
-#pragma unroll
-      for (int j = 0; j < NV; j++) acc = fmaf(Mi[j], s.J[e][j], acc);
-    }
-    X[e] = acc;
-  }
   const int li = lane < NV ? lane : 0;
   const float lm = lane < NV ? 1.f : 0.f;
-  // pair constants A11, A22, A12
+  wsync();
+  // X[e][k] = (inv(M) J_e')_k for pyramidal dense rows (LDS, overlays dead stage arrays)
+  for (int e = 0; e < ndense; e++) {
+    if (s.efc_type[nsparse + e] != C_CON_PYRAMIDAL) continue;
+    float acc = 0.f;
 #pragma unroll
-  for (int e = 0; e + 1 < MAXDENSE; e++) {
-    if (e < ndense - 1 && s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1) {
-      float j1 = lm * s.J[e][li], j2 = lm * s.J[e + 1][li];
-      float a11 = wave_sum(j1 * X[e]), a22 = wave_sum(j2 * X[e + 1]), a12 = wave_sum(j1 * X[e + 1]);
-      if (lane == 0) { s.ns_a[e][0] = a11; s.ns_a[e][1] = a22; s.ns_a[e][2] = a12; }
-    }
+    for (int j = 0; j < NV; j++) acc = fmaf(Mi[j], s.J[e][j], acc);
+    if (lane < NV) s.X[e][lane] = acc;
+  }
+  wsync();
+  // pair constants A11, A22, A12 of each opposing edge pair
+  for (int e = 0; e + 1 < ndense; e++) {
+    if (!(s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1)) continue;
+    float j1 = lm * s.J[e][li], j2 = lm * s.J[e + 1][li];
+    float x1 = lm * s.X[e][li], x2 = lm * s.X[e + 1][li];
+    float a11 = wave_sum(j1 * x1), a22 = wave_sum(j2 * x2), a12 = wave_sum(j1 * x2);
+    if (lane == 0) { s.ns_a[e][0] = a11; s.ns_a[e][1] = a22; s.ns_a[e][2] = a12; }
   }
   // forces: frictionloss rows per dof lane, dense rows per lane
   float ffl = 0.f, fd = 0.f;
@@ -540,12 +543,12 @@ __device__ void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mr
       qacc = fmaf(Mi[d], delta, qacc);
       if (lane == d) ffl = x;
     }
-#pragma unroll
-    for (int e = 0; e + 1 < MAXDENSE; e++) {
-      if (!(e < ndense - 1 && s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1)) continue;
+    for (int e = 0; e + 1 < ndense; e++) {
+      if (!(s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1)) continue;
       float A11 = s.ns_a[e][0], A22 = s.ns_a[e][1], A12 = s.ns_a[e][2];
       float K = A11 + A22 - 2.f * A12;
       if (K < MINVAL) continue;
+      float x1 = lm * s.X[e][li], x2 = lm * s.X[e + 1][li];
       float r1 = wave_sum(lm * s.J[e][li] * qacc) - s.efc_aref[nsparse + e];
       float r2 = wave_sum(lm * s.J[e + 1][li] * qacc) - s.efc_aref[nsparse + e + 1];
       float f1 = rlane(fd, e), f2 = rlane(fd, e + 1);
@@ -554,7 +557,7 @@ __device__ void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mr
       float d1 = 0.5f * (sum + xn) - f1, d2 = 0.5f * (sum - xn) - f2;
       if (d1 == 0.f && d2 == 0.f) continue;
       impr -= r1 * d1 + r2 * d2 + 0.5f * (A11 * d1 * d1 + 2.f * A12 * d1 * d2 + A22 * d2 * d2);
-      qacc = fmaf(X[e], d1, fmaf(X[e + 1], d2, qacc));
+      qacc = fmaf(x1, d1, fmaf(x2, d2, qacc));
       if (lane == e) fd = f1 + d1;
       if (lane == e + 1) fd = f2 + d2;
     }
@@ -567,7 +570,7 @@ __device__ void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mr
 
 // ---------------------------------------------------------------------------------------
 // mju_rayGeom for site shapes: distance to the first crossing at t >= 0, or -1
-__device__ float ray_geom(const float* pos, const float* mat, const float* size, const float* pnt,
+AW_DEV float ray_geom(const float* pos, const float* mat, const float* size, const float* pnt,
                           const float* vec, int type) {
   float dif[3], lp[3], lv[3];
   sub3(dif, pnt, pos);
@@ -623,7 +626,7 @@ __device__ float ray_geom(const float* pos, const float* mat, const float* size,
 }
 
 // touch sensors of the task (mj_sensorAcc, mjSENS_TOUCH)
-__device__ void stage_touch(const DModel& m, Env& s, int lane) {
+AW_DEV void stage_touch(const DModel& m, Env& s, int lane) {
   for (int t = 0; t < m.ntouch; t++) {
     int site = m.touch_site[t], bid = m.site_bodyid[site];
     float val = 0.f;

@@ -13,7 +13,7 @@
 
 namespace aw {
 
-__device__ __forceinline__ void quat2euler(const float* q, float* e) {
+AW_DEV void quat2euler(const float* q, float* e) {
   float w = q[0], x = q[1], y = q[2], z = q[3];
   float Nq = w * w + x * x + y * y + z * z;
   float m[9];
@@ -36,7 +36,7 @@ __device__ __forceinline__ void quat2euler(const float* q, float* e) {
 }
 
 // utils/quatmath.py:60-76 (reference convention)
-__device__ __forceinline__ void euler2quat_ref(const float* eu, float* q) {
+AW_DEV void euler2quat_ref(const float* eu, float* q) {
   float ai = eu[2] / 2, aj = -eu[1] / 2, ak = eu[0] / 2;
   float si = sinf(ai), sj = sinf(aj), sk = sinf(ak);
   float ci = cosf(ai), cj = cosf(aj), ck = cosf(ak);
@@ -47,14 +47,14 @@ __device__ __forceinline__ void euler2quat_ref(const float* eu, float* q) {
   q[1] = cj * cs - sj * sc;
 }
 
-__device__ __forceinline__ float dist3(const float* a, const float* b) {
+AW_DEV float dist3(const float* a, const float* b) {
   float d[3];
   sub3(d, a, b);
   return norm3(d);
 }
 
 // writes obs[0..obs_dim) into s.rowbuf (LDS); lane-parallel qpos copies
-__device__ void task_obs(const DModel& m, Env& s, int lane, float* out) {
+AW_DEV void task_obs(const DModel& m, Env& s, int lane, float* out) {
   const int* id = m.task_idx;
   const int nq = m.nq, nv = m.nv;
   switch (m.task_kind) {
@@ -123,7 +123,7 @@ __device__ void task_obs(const DModel& m, Env& s, int lane, float* out) {
 }
 
 // lane 0 computes reward / done / goal (fp32 restatement of the reference arithmetic)
-__device__ void task_reward(const DModel& m, Env& s, float* reward, int* done, int* goal) {
+AW_DEV void task_reward(const DModel& m, Env& s, float* reward, int* done, int* goal) {
   const int* id = m.task_idx;
   float r = 0.f;
   *done = 0;
@@ -203,7 +203,7 @@ __device__ void task_reward(const DModel& m, Env& s, float* reward, int* done, i
 
 // ---------------------------------------------------------------------------------------
 // Philox4x32-10 counter-based RNG
-__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+AW_DEV void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int i = 0; i < 10; i++) {
     uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
@@ -213,18 +213,20 @@ __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) 
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
 }
-__device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+AW_DEV float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
 
 // reset draws -> params (tasks.draws_to_params); counter = (env, episode, stream 0x5EED, block)
-__device__ void sample_params(const DModel& m, uint64_t seed, uint32_t genv, uint32_t episode, float* params) {
+AW_DEV void sample_params(const DModel& m, uint64_t seed, uint32_t genv, uint32_t episode, float* params) {
   float u[8];
+#pragma unroll
   for (int blk = 0; blk < 2; blk++) {
     uint32_t c[4] = {genv, episode, 0x5EEDu, (uint32_t)blk};
     philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
     for (int k = 0; k < 4; k++) u[4 * blk + k] = u01(c[k]);
   }
   float d[8];
-  for (int k = 0; k < m.ndraw; k++) d[k] = m.draw_lo[k] + (m.draw_hi[k] - m.draw_lo[k]) * u[k];
+#pragma unroll
+  for (int k = 0; k < 8; k++) d[k] = k < m.ndraw ? m.draw_lo[k] + (m.draw_hi[k] - m.draw_lo[k]) * u[k] : 0.f;
   if (m.task_kind == 2) {
     float eu[3] = {d[0], d[1], 0.f};
     euler2quat_ref(eu, params);
@@ -233,7 +235,9 @@ __device__ void sample_params(const DModel& m, uint64_t seed, uint32_t genv, uin
     params[1] = d[1];
     params[2] = -0.14f - (-0.24f - d[1]);
   } else {
-    for (int k = 0; k < m.nparam; k++) params[k] = d[k];
+#pragma unroll
+    for (int k = 0; k < MAXP; k++)
+      if (k < m.nparam) params[k] = d[k];
   }
 }
 
