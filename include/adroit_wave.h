@@ -117,6 +117,11 @@ int aw_task_eval(aw_handle* h, int n, const float* qpos, const float* qvel, cons
 #define AW_DUMP_SIZE 2728
 int aw_forward_dump(aw_handle* h, int env, const float* ctrl, float* out, void* stream);
 
+/* Diagnostic: per-stage shader-clock cycles of k_step summed over all waves since the last
+ * reset (16 counters, see aw_common.h PR_*).  Only libraries built with -DAW_STAGE_PROF
+ * collect them; the product build returns AW_EUNSUPPORTED. */
+int aw_stage_profile(unsigned long long* out, int reset);
+
 const char* aw_last_error(void);
 
 #ifdef __cplusplus

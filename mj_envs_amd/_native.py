@@ -14,7 +14,8 @@ from typing import Optional
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libadroit_hip.so")
+# AW_LIB selects a diagnostic build (e.g. libadroit_hip_prof.so with the stage profiler)
+LIB_PATH = os.environ.get("AW_LIB") or os.path.join(HERE, "libadroit_hip.so")
 
 AW_NDIMS = 13
 AW_DUMP_SIZE = 2728
@@ -55,9 +56,10 @@ def load():
     L.aw_episode_stats.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp]
     L.aw_task_eval.argtypes = [_vp, ctypes.c_int] + [_vp] * 10 + [_vp]
     L.aw_forward_dump.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp]
+    L.aw_stage_profile.argtypes = [_vp, ctypes.c_int]
     for f in ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "aw_step",
               "aw_random_actions", "aw_get_state", "aw_set_state", "aw_status", "aw_episode_stats",
-              "aw_task_eval", "aw_forward_dump"):
+              "aw_task_eval", "aw_forward_dump", "aw_stage_profile"):
         getattr(L, f).restype = ctypes.c_int
     _lib = L
     return L
@@ -65,7 +67,24 @@ def load():
 
 EXPORTS = ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "aw_step",
            "aw_random_actions", "aw_get_state", "aw_set_state", "aw_status", "aw_episode_stats",
-           "aw_task_eval", "aw_forward_dump", "aw_last_error")
+           "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_last_error")
+
+STAGES = ("pre", "kinematics", "collision", "com_crb", "rne_smooth_solve", "constraints", "newton",
+          "noslip", "jt_touch", "euler", "task_obs", "reset", "checks")
+SUBSTAGES = ("nt_init", "nt_hess", "nt_chol", "nt_solve", "nt_ls", "nt_upd", "ns_minv", "ns_setup", "ns_iter")
+
+
+def stage_profile(reset: bool = True) -> dict:
+    """Per-stage shader-clock cycles of k_step (diagnostic build only, see aw_stage_profile)."""
+    buf = (ctypes.c_ulonglong * 32)()
+    _check(load().aw_stage_profile(buf, int(reset)))
+    v = list(buf)
+    out = {name: v[i] for i, name in enumerate(STAGES)}
+    out["waves"], out["substeps"] = v[13], v[14]
+    out["newton_iters"], out["noslip_iters"], out["nefc"], out["ncon"] = v[15], v[16], v[17], v[18]
+    for i, name in enumerate(SUBSTAGES):
+        out[name] = v[19 + i]
+    return out
 
 
 def _check(rc: int):
@@ -166,7 +185,8 @@ class Sim:
         res["qM"] = res["qM"][:nv * nv].reshape(nv, nv)
         sc = res["scalars"]
         ncon, nefc = int(sc[0]), int(sc[1])
-        res.update(ncon=ncon, nefc=nefc, nsparse=int(sc[2]), ndense=int(sc[3]), touch=sc[4], status=int(sc[5]))
+        res.update(ncon=ncon, nefc=nefc, nsparse=int(sc[2]), ndense=int(sc[3]), touch=sc[4], status=int(sc[5]),
+                   solver_iter=int(sc[6]), noslip_iter=int(sc[7]))
         res["con_dist"] = res["con_dist"][:ncon]
         res["con_pos"] = res["con_pos"][:3 * ncon].reshape(ncon, 3)
         res["con_frame"] = res["con_frame"][:9 * ncon].reshape(ncon, 9)

@@ -21,6 +21,10 @@
 
 using namespace aw;
 
+#ifdef AW_STAGE_PROF
+__device__ unsigned long long g_stage_prof[AW_NPROF];
+#endif
+
 // ---------------------------------------------------------------------------------------
 // device-side state owned by the handle
 struct DState {
@@ -85,9 +89,12 @@ AW_DEV void stage_collision(const DModel& m, Env& s, int lane) {
 template <int NV>
 AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
   stage_kinematics(m, s, lane);
+  AW_PROF(s, PR_KIN);
   stage_collision(m, s, lane);
+  AW_PROF(s, PR_COLL);
   stage_com(m, s, lane);
   stage_crb<NV>(m, s, lane, Mrow);
+  AW_PROF(s, PR_CRB);
   stage_velocity(m, s, lane);
   // qacc_smooth = M \ qfrc_smooth
   {
@@ -95,7 +102,7 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
 #pragma unroll
     for (int k = 0; k < NV; k++) row[k] = Mrow[k];
     float invd = 1.f;
-    chol_factor<NV>(row, lane, invd);
+    chol_factor<NV>(row, lane, invd, s);
     chol_store<NV>(row, lane, s);
     wsync();
     float fs = lane < NV ? s.qfrc_smooth[lane] : 0.f;
@@ -103,7 +110,10 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
     if (lane < NV) s.qacc_smooth[lane] = x;
     wsync();
   }
+  AW_PROF(s, PR_SMOOTH);
+  if (lane == 0) { s.it_newton = 0; s.it_noslip = 0; }
   stage_constraints<NV>(m, s, lane);
+  AW_PROF(s, PR_CONSTR);
   if (s.nefc == 0) {
     if (lane < NV) { s.qacc[lane] = s.qacc_smooth[lane]; s.qfrc_con[lane] = 0.f; }
     wsync();
@@ -111,10 +121,12 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
     float a = 0.f;
 #ifndef X_NONEWTON
     solve_newton<NV>(m, s, lane, Mrow, a);
+    AW_PROF(s, PR_NEWTON);
 #endif
     
 #ifndef X_NONOSLIP
     if (m.noslip_iterations > 0 && !(m.disableflags & DSBL_NOSLIP)) solve_noslip<NV>(m, s, lane, Mrow, a);
+    AW_PROF(s, PR_NOSLIP);
 #endif
     for (int r = lane; r < s.nefc; r += 64) s.rowbuf[r] = s.efc_force[r];
     wsync();
@@ -123,6 +135,7 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
     wsync();
   }
   stage_touch(m, s, lane);
+  AW_PROF(s, PR_JT_TOUCH);
 }
 
 // mj_Euler: implicit joint damping, semi-implicit positions, warmstart <- qacc
@@ -137,7 +150,7 @@ AW_DEV void euler(const DModel& m, Env& s, int lane, const float (&Mrow)[NV]) {
 #pragma unroll
     for (int k = 0; k < NV; k++) row[k] = Mrow[k] + (k == lane ? dd : 0.f);
     float invd = 1.f;
-    chol_factor<NV>(row, lane, invd);
+    chol_factor<NV>(row, lane, invd, s);
     chol_store<NV>(row, lane, s);
     wsync();
     float f = lane < NV ? s.qfrc_smooth[lane] + s.qfrc_con[lane] : 0.f;
@@ -256,6 +269,7 @@ __global__ void __launch_bounds__(64) k_step(DModel m, DState st, int n, const f
   __shared__ Env s;
   const int env = blockIdx.x, lane = threadIdx.x;
   if (env >= n) return;
+  AW_PROF_START(s);
   load_env<NV>(m, s, st, env, lane);
   if (lane < m.nu) {
     float a = clampf(actions[(size_t)env * m.nu + lane], -1.f, 1.f);
@@ -266,14 +280,18 @@ __global__ void __launch_bounds__(64) k_step(DModel m, DState st, int n, const f
   float* ob = obs + (size_t)env * m.obs_dim;
   int sub = 0;
   bool resetting = false, retry = false;
+  AW_PROF(s, PR_PRE);
 #pragma nounroll
   while (true) {
     if (!resetting && !retry) check_state<NV>(s, lane);
+    AW_PROF(s, PR_CHECK);
     forward<NV>(m, s, lane, Mrow);
     if (resetting) break;
     if (!retry && check_acc<NV>(s, lane)) { retry = true; continue; }
     retry = false;
     euler<NV>(m, s, lane, Mrow);
+    AW_PROF(s, PR_EULER);
+    AW_PROF_COUNT(s, PR_SUBSTEPS);
     if (++sub < m.frame_skip) continue;
     // env-step complete: observation, reward, episode bookkeeping
     write_obs(m, s, lane, ob);
@@ -302,6 +320,7 @@ __global__ void __launch_bounds__(64) k_step(DModel m, DState st, int n, const f
       }
     }
     store_env<NV>(m, s, st, env, lane);
+    AW_PROF(s, PR_TASK);
     int ended = __shfl(term | trunc, 0, 64);
     if (!(autoreset && ended)) break;
     __threadfence_block();
@@ -309,12 +328,19 @@ __global__ void __launch_bounds__(64) k_step(DModel m, DState st, int n, const f
       for (int o = lane; o < m.obs_dim; o += 64) terminal_obs[(size_t)env * m.obs_dim + o] = s.rowbuf[o];
     wsync();
     reset_prepare<NV>(m, s, st, env, lane, nullptr, seed);
+    AW_PROF(s, PR_RESET);
     resetting = true;
   }
   if (resetting) {
     write_obs(m, s, lane, ob);
     store_env<NV>(m, s, st, env, lane);
   }
+#ifdef AW_STAGE_PROF
+  AW_PROF(s, PR_TASK);
+  AW_PROF_COUNT(s, PR_CALLS);
+  if (lane == 0)
+    for (int i = 0; i < AW_NPROF; i++) atomicAdd(&g_stage_prof[i], s.prof_acc[i]);
+#endif
 }
 
 template <int NV>
@@ -378,6 +404,7 @@ __global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const
   if (lane == 0) {
     out[1760] = (float)s.ncon; out[1761] = (float)s.nefc; out[1762] = (float)s.nsparse;
     out[1763] = (float)s.ndense; out[1764] = s.touch[0]; out[1765] = (float)s.status;
+    out[1766] = (float)s.it_newton; out[1767] = (float)s.it_noslip;
   }
   if (lane < MAXCON) {
     bool v = lane < s.ncon;
@@ -903,6 +930,20 @@ int aw_forward_dump(aw_handle* h, int env, const float* ctrl, float* out, void* 
 #undef CALL
   HIPCHK(hipGetLastError());
   return AW_OK;
+}
+
+int aw_stage_profile(unsigned long long* out, int reset) {
+#ifdef AW_STAGE_PROF
+  if (out) HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_prof), sizeof(unsigned long long) * AW_NPROF));
+  if (reset) {
+    unsigned long long z[AW_NPROF] = {};
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stage_prof), z, sizeof(z)));
+  }
+  return AW_OK;
+#else
+  (void)out; (void)reset;
+  return fail(AW_EUNSUPPORTED, "library built without -DAW_STAGE_PROF");
+#endif
 }
 
 }  // extern "C"

@@ -31,6 +31,42 @@ constexpr int MAXPAIRCON = 8; // contacts per geom pair
 
 constexpr float MINVAL = 1e-15f;
 
+// Stage profiler (diagnostic builds only, -DAW_STAGE_PROF): shader-clock cycles per stage,
+// summed over waves; read back through aw_stage_profile().
+constexpr int AW_NPROF = 32;
+enum {
+  PR_PRE = 0, PR_KIN, PR_COLL, PR_CRB, PR_SMOOTH, PR_CONSTR, PR_NEWTON, PR_NOSLIP, PR_JT_TOUCH,
+  PR_EULER, PR_TASK, PR_RESET, PR_CHECK, PR_CALLS, PR_SUBSTEPS,
+  PR_NEWTON_IT, PR_NOSLIP_IT, PR_NEFC, PR_NCON,
+  PR_NT_INIT, PR_NT_HESS, PR_NT_CHOL, PR_NT_SOLVE, PR_NT_LS, PR_NT_UPD, PR_NS_MINV, PR_NS_SETUP, PR_NS_ITER
+};
+#ifdef AW_STAGE_PROF
+#define AW_PROF_START(S)                                            \
+  do {                                                              \
+    unsigned long long _t = __builtin_amdgcn_s_memtime();           \
+    if (threadIdx.x == 0) {                                         \
+      for (int _i = 0; _i < AW_NPROF; _i++) (S).prof_acc[_i] = 0;   \
+      (S).prof_t = _t;                                              \
+    }                                                               \
+  } while (0)
+#define AW_PROF(S, ID)                                              \
+  do {                                                              \
+    __syncthreads();                                                \
+    unsigned long long _t = __builtin_amdgcn_s_memtime();           \
+    if (threadIdx.x == 0) {                                         \
+      (S).prof_acc[ID] += _t - (S).prof_t;                          \
+      (S).prof_t = _t;                                              \
+    }                                                               \
+  } while (0)
+#define AW_PROF_COUNT(S, ID) do { if (threadIdx.x == 0) (S).prof_acc[ID] += 1; } while (0)
+#define AW_PROF_ADD(S, ID, V) do { if (threadIdx.x == 0) (S).prof_acc[ID] += (unsigned long long)(V); } while (0)
+#else
+#define AW_PROF_START(S) ((void)0)
+#define AW_PROF(S, ID) ((void)0)
+#define AW_PROF_COUNT(S, ID) ((void)0)
+#define AW_PROF_ADD(S, ID, V) ((void)0)
+#endif
+
 enum { GEOM_PLANE = 0, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_CYLINDER = 5, GEOM_BOX = 6 };
 enum { JNT_SLIDE = 2, JNT_HINGE = 3 };
 enum { C_FRIC_DOF = 0, C_FRIC_TEN = 1, C_LIM_JNT = 2, C_LIM_TEN = 3, C_CON_FRICTIONLESS = 4, C_CON_PYRAMIDAL = 5 };
@@ -133,6 +169,7 @@ struct __attribute__((aligned(16))) Env {
   float txmat[MAXTOUCH][9];
   float tlen[MAXT];
   float L[MAXV][VS];      // Cholesky rows (M, then H, then M + hD); also sparse-H staging
+  float4 colbuf[16];      // Cholesky column broadcast (64 floats, 16-byte aligned for b128 reads)
   // contacts
   int ncon;
   int con_key[MAXCON], con_pair[MAXCON], con_efc[MAXCON];
@@ -149,6 +186,11 @@ struct __attribute__((aligned(16))) Env {
   float ns_a[MAXDENSE][3];   // noslip: per pyramid edge pair A11, A22, A12 (stored at first edge)
   float touch[MAXTOUCH];
   unsigned status;
+  int it_newton, it_noslip;   // iterations of the last solve (introspection)
+#ifdef AW_STAGE_PROF
+  unsigned long long prof_acc[AW_NPROF];
+  unsigned long long prof_t;
+#endif
   int red_i;
   float red_f[4];
 };
@@ -159,17 +201,42 @@ AW_DEV float rlane(float x, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
 }
 AW_DEV int rlane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
-AW_DEV void wsync() { __syncthreads(); }
+// Intra-wave LDS hand-off.  Every workgroup is exactly one wave64: LDS operations of a wave
+// execute in issue order, so cross-lane communication through LDS needs only a compiler-level
+// ordering point, not s_barrier + a full s_waitcnt drain (which would serialise every
+// outstanding load at each hand-off).  A wavefront-scope fence emits no instruction.
+AW_DEV void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
 
+// DPP butterfly reductions (VALU only: no LDS round trip as __shfl_xor / ds_bpermute would
+// take).  quad_perm [1,0,3,2] and [2,3,0,1], row_half_mirror and row_mirror leave every lane of
+// a 16-lane row holding the row total; row_bcast15 (rows 1,3) and row_bcast31 (rows 2,3) fold
+// the rows so lane 63 holds the wave total, which readlane broadcasts (uniform result).
+template <int CTRL, int ROWMASK = 0xF>
+AW_DEV float dpp_f(float old, float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old),
+                                                               __builtin_bit_cast(int, x), CTRL, ROWMASK, 0xF, false));
+}
 AW_DEV float wave_sum(float x) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
-  return x;
+  x += dpp_f<0xB1>(0.f, x);
+  x += dpp_f<0x4E>(0.f, x);
+  x += dpp_f<0x141>(0.f, x);
+  x += dpp_f<0x140>(0.f, x);
+  x += dpp_f<0x142, 0xA>(0.f, x);
+  x += dpp_f<0x143, 0xC>(0.f, x);
+  return rlane(x, 63);
 }
 AW_DEV float wave_max(float x) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
-  return x;
+  constexpr float NEG = -3.402823466e38f;
+  x = fmaxf(x, dpp_f<0xB1>(NEG, x));
+  x = fmaxf(x, dpp_f<0x4E>(NEG, x));
+  x = fmaxf(x, dpp_f<0x141>(NEG, x));
+  x = fmaxf(x, dpp_f<0x140>(NEG, x));
+  x = fmaxf(x, dpp_f<0x142, 0xA>(NEG, x));
+  x = fmaxf(x, dpp_f<0x143, 0xC>(NEG, x));
+  return rlane(x, 63);
 }
 // exclusive prefix sum of small non-negative ints across the wave
 AW_DEV int wave_excl_scan(int x, int lane, int* total) {

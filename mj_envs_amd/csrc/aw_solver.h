@@ -17,20 +17,36 @@
 namespace aw {
 
 // ---------------------------------------------------------------------------------------
-// dense Cholesky of a lane-distributed SPD matrix (lane i holds row i; lower part used)
+// dense Cholesky of a lane-distributed SPD matrix (lane i holds row i; lower part used).
+// Right-looking: column j is scaled in registers, published once through LDS, and every lane
+// pulls the column back with 16-byte broadcast reads for its rank-1 update.  Entries above a
+// lane's diagonal (and rows of lanes >= NV) take unmasked garbage updates that are never read:
+// the factor proper is the lower triangle of lanes < NV.
 template <int NV>
-AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd) {
+AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
+  float* col = reinterpret_cast<float*>(s.colbuf);
 #pragma unroll
   for (int j = 0; j < NV; j++) {
-    float djj = rlane(row[j], j);
-    float sq = sqrtf(fmaxf(djj, MINVAL));
-    float inv = 1.0f / sq;
-    if (lane == j) { row[j] = sq; invd = inv; }
-    else if (lane > j) row[j] *= inv;
+    const float djj = rlane(row[j], j);
+    const float sq = sqrtf(fmaxf(djj, MINVAL));
+    const float inv = 1.0f / sq;
+    row[j] = lane == j ? sq : row[j] * inv;
+    if (lane == j) invd = inv;
+    if (j + 1 < NV) {
+      col[lane] = row[j];
+      wsync();
+      const float lij = row[j];
 #pragma unroll
-    for (int k = j + 1; k < NV; k++) {
-      float lkj = rlane(row[j], k);
-      if (lane >= k) row[k] = fmaf(-row[j], lkj, row[k]);
+      for (int q = (j + 1) >> 2; q <= (NV - 1) >> 2; q++) {
+        const float4 c = s.colbuf[q];
+        const float cv[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+          const int k = 4 * q + t;
+          if (k > j && k < NV) row[k] = fmaf(-lij, cv[t], row[k]);
+        }
+      }
+      wsync();
     }
   }
 }
@@ -294,6 +310,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
 
 // ---------------------------------------------------------------------------------------
 // Newton solver
+constexpr float GRAD_NOISE = 2e-6f;   // ~16 fp32 ulps of the gradient's terms
 struct RowR {
   float D, floss, Jaref, Jp, force;
   int st, fr, valid;
@@ -356,13 +373,16 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
     if (cw < cost) cost = cw;
     else { set_point(a0); cost = eval(); }
   }
+  float gref = 0.f;   // |Ma|^2 + |fs|^2 + |J'f|^2 per lane: the fp32 noise scale of the gradient
   auto gradient = [&]() {
     for (int h = 0; h < 2; h++) { int r = lane + 64 * h; if (r < nefc) s.rowbuf[r] = rr[h].force; }
     wsync();
     float jf = jt_mul<NV>(s, lane);
+    gref = lane < NV ? Ma * Ma + fs * fs + jf * jf : 0.f;
     return lane < NV ? Ma - fs - jf : 0.f;
   };
   float grad = gradient();
+  AW_PROF(s, PR_NT_INIT);
   int iter = 0;
   for (; iter < m.iterations; iter++) {
     // Hessian H = M + J' D_quad J
@@ -397,11 +417,14 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
       for (int k = 0; k < NV; k++) H[k] = fmaf(av, s.J[d][k], H[k]);
     }
     wsync();
+    AW_PROF(s, PR_NT_HESS);
     float invd = 1.f;
-    chol_factor<NV>(H, lane, invd);
+    chol_factor<NV>(H, lane, invd, s);
     chol_store<NV>(H, lane, s);
     wsync();
+    AW_PROF(s, PR_NT_CHOL);
     float p = -chol_solve<NV>(H, invd, grad, lane, s);
+    AW_PROF(s, PR_NT_SOLVE);
     // exact line search on the piecewise-quadratic 1-D cost
     float Mp = matvec<NV>(Mrow, p);
     float c0 = wave_sum(lane < NV ? p * (Ma - fs) : 0.f);
@@ -442,6 +465,7 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
         if (fabsf(d1) <= tol) break;
       }
     }
+    AW_PROF(s, PR_NT_LS);
     if (alpha == 0.f) { iter++; break; }
     a += alpha * p;
     Ma += alpha * Mp;
@@ -451,8 +475,17 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
     grad = gradient();
     float gn = sqrtf(wave_sum(grad * grad));
     float improvement = scale * (oldcost - cost), gradnorm = scale * gn;
+    // fp32 termination: a gradient at the rounding floor of its own terms (Ma, qfrc_smooth,
+    // J'f) cannot shrink further -- the fp64 reference would already stop on its 1e-8 test
+    // here; an extra Newton step in fp32 only re-solves the same active set.
+    if (gn <= GRAD_NOISE * sqrtf(wave_sum(gref))) { iter++; break; }
+    AW_PROF(s, PR_NT_UPD);
     if (improvement < m.tolerance || gradnorm < m.tolerance) { iter++; break; }
   }
+  if (lane == 0) s.it_newton = iter;
+  AW_PROF_ADD(s, PR_NEWTON_IT, iter);
+  AW_PROF_ADD(s, PR_NEFC, nefc);
+  AW_PROF_ADD(s, PR_NCON, s.ncon);
   for (int h = 0; h < 2; h++) {
     int r = lane + 64 * h;
     if (r < nefc) s.efc_force[r] = rr[h].force;
@@ -473,7 +506,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
 #pragma unroll
     for (int k = 0; k < NV; k++) row[k] = Mrow[k];
     float invd = 1.f;
-    chol_factor<NV>(row, lane, invd);
+    chol_factor<NV>(row, lane, invd, s);
     chol_store<NV>(row, lane, s);
     if (lane < NV) s.vec2[lane] = invd;
     wsync();
@@ -501,6 +534,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
   const int li = lane < NV ? lane : 0;
   const float lm = lane < NV ? 1.f : 0.f;
   wsync();
+  AW_PROF(s, PR_NS_MINV);
   // X[e][k] = (inv(M) J_e')_k for pyramidal dense rows (LDS, overlays dead stage arrays)
   for (int e = 0; e < ndense; e++) {
     if (s.efc_type[nsparse + e] != C_CON_PYRAMIDAL) continue;
@@ -519,30 +553,53 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
     if (lane == 0) { s.ns_a[e][0] = a11; s.ns_a[e][1] = a22; s.ns_a[e][2] = a12; }
   }
   // forces: frictionloss rows per dof lane, dense rows per lane
+  const bool use_fl = !(m.disableflags & DSBL_FRICTIONLOSS);
   float ffl = 0.f, fd = 0.f;
-  if (lane < NV && m.fl_row[lane] >= 0 && m.fl_row[lane] < nsparse) ffl = s.efc_force[m.fl_row[lane]];
+  // per-dof-lane constants of the frictionloss row of that dof (lane d owns row fl_row[d])
+  float fl_aref = 0.f, fl_lim = 0.f, fl_A = 1.f, fl_invA = 0.f;
+  bool fl_ok;
+  {
+    float dg = 0.f;   // inv(M)[lane][lane]
+#pragma unroll
+    for (int k = 0; k < NV; k++) dg = k == lane ? Mi[k] : dg;
+    const int row = lane < NV ? m.fl_row[lane] : -1;
+    const bool has = row >= 0 && row < nsparse;
+    if (has) ffl = s.efc_force[row];
+    fl_ok = use_fl && has && dg >= MINVAL;
+    if (fl_ok) {
+      fl_aref = s.efc_aref[row];
+      fl_lim = s.efc_floss[row];
+      fl_A = dg;
+      fl_invA = 1.0f / dg;
+    }
+  }
   if (lane < ndense) fd = s.efc_force[nsparse + lane];
   wsync();
   qacc = lane < NV ? qacc : 0.f;
   const float scale = 1.f / (m.meaninertia * (float)(NV > 1 ? NV : 1));
-  const bool use_fl = !(m.disableflags & DSBL_FRICTIONLOSS);
+  AW_PROF(s, PR_NS_SETUP);
+  if (lane == 0) s.it_noslip = 0;
   for (int it = 0; it < m.noslip_iterations; it++) {
+    AW_PROF_ADD(s, PR_NOSLIP_IT, 1);
+    if (lane == 0) s.it_noslip = it + 1;
     float impr = 0.f;
+    // dry-friction rows in dof order (Gauss-Seidel).  Every lane evaluates the projected update
+    // of its own row against the current qacc; step d keeps lane d's.  Lanes without an
+    // active row propose exactly zero (branch-free).
+    float imp_l = 0.f;
 #pragma unroll
     for (int d = 0; d < NV; d++) {
-      int row = m.fl_row[d];
-      if (!use_fl || row < 0 || row >= nsparse) continue;
-      float Add = rlane(Mi[d], d);
-      if (Add < MINVAL) continue;
-      float r = rlane(qacc, d) - s.efc_aref[row];
-      float f = rlane(ffl, d), fl = s.efc_floss[row];
-      float x = clampf(f - r / Add, -fl, fl);
-      float delta = x - f;
-      if (delta == 0.f) continue;
-      impr -= r * delta + 0.5f * Add * delta * delta;
+      const float r = qacc - fl_aref;
+      const float x = fminf(fmaxf(fmaf(-r, fl_invA, ffl), -fl_lim), fl_lim);
+      const float dl = fl_ok ? x - ffl : 0.f;
+      const float delta = rlane(dl, d);
+      if (lane == d) {
+        imp_l += r * dl + 0.5f * fl_A * dl * dl;
+        ffl = fl_ok ? x : ffl;
+      }
       qacc = fmaf(Mi[d], delta, qacc);
-      if (lane == d) ffl = x;
     }
+    impr -= wave_sum(imp_l);
     for (int e = 0; e + 1 < ndense; e++) {
       if (!(s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1)) continue;
       float A11 = s.ns_a[e][0], A22 = s.ns_a[e][1], A12 = s.ns_a[e][2];
@@ -563,6 +620,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
     }
     if (impr * scale < m.noslip_tolerance) break;
   }
+  AW_PROF(s, PR_NS_ITER);
   if (lane < NV && m.fl_row[lane] >= 0 && m.fl_row[lane] < nsparse) s.efc_force[m.fl_row[lane]] = ffl;
   if (lane < ndense) s.efc_force[nsparse + lane] = fd;
   wsync();

@@ -1,0 +1,276 @@
+"""Gym-style facades over the batched HIP simulator.
+
+Two ways in, both backed by the same C-ABI (``include/adroit_wave.h``) and nothing else:
+
+* ``HammerEnvV0`` / ``DoorEnvV0`` / ``PenEnvV0`` / ``RelocateEnvV0`` -- one env per object with
+  the reference's per-env API (``hand_manipulation_suite/*_v0.py``): ``step(a) -> (obs, reward,
+  done, {'goal_achieved'})``, ``reset() -> (obs, {})``, ``get_obs``, ``get_env_state`` /
+  ``set_env_state`` (same dict keys), ``evaluate_success(paths)``, ``act_mid`` / ``act_rng``,
+  ``frame_skip``, ``action_space`` / ``observation_space``.  numpy in, numpy out.
+* ``AdroitVecEnv`` -- N envs of one task on one GPU, torch device tensors in and out, in-kernel
+  auto-reset, 5-tuple ``(obs, reward, terminated, truncated, info)`` like the reference's
+  ``CustomPixelObservationWrapper`` (``wrappers.py:32-76``) hands to its trainers.
+
+Model-parameter resets (nail-board height, door frame position, pen target orientation,
+relocate object / target) are per-env override vectors (``tasks.param_layout``), so envs in one
+batch never share mutated model state.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from . import _native
+from .tasks import TASKS, attach_task, load_model, param_layout
+
+
+class Box:
+    """Minimal stand-in for ``gym.spaces.Box`` (gym is not a dependency of the hot path)."""
+
+    def __init__(self, low, high, shape, dtype=np.float32):
+        self.shape = tuple(shape)
+        self.dtype = np.dtype(dtype)
+        self.low = np.full(self.shape, low, self.dtype)
+        self.high = np.full(self.shape, high, self.dtype)
+
+    def sample(self, rng: Optional[np.random.Generator] = None):
+        rng = rng or np.random.default_rng()
+        return rng.uniform(self.low, self.high).astype(self.dtype)
+
+    def contains(self, x) -> bool:
+        x = np.asarray(x)
+        return x.shape == self.shape and bool(np.all(x >= self.low) and np.all(x <= self.high))
+
+
+def _evaluate_success(env_id: str, paths: List[dict]) -> float:
+    """``hammer_v0.py:167-175`` (and door/pen/relocate): % of paths with > k goal steps."""
+    k = TASKS[env_id].success_steps
+    if not paths:
+        return 0.0
+    n = sum(1 for p in paths if np.sum(p["env_infos"]["goal_achieved"]) > k)
+    return n * 100.0 / len(paths)
+
+
+class AdroitVecEnv:
+    """``num_envs`` envs of ``env_id`` on GPU ``device``; every buffer stays in HBM."""
+
+    def __init__(self, env_id: str, num_envs: int, device: int = 0, variation_type: Optional[str] = None,
+                 seed: int = 1, autoreset: bool = True):
+        import torch
+        self.env_id = env_id
+        self.spec = TASKS[env_id]
+        self.model = attach_task(load_model(env_id), env_id, variation_type)
+        self.variation_type = variation_type
+        self.sim = _native.Sim(self.model.to_blob(), num_envs, device)
+        self.num_envs = num_envs
+        self.seed = int(seed)
+        self.autoreset = autoreset
+        s = self.sim
+        self.nq, self.nv, self.nu, self.obs_dim, self.nparam = s.nq, s.nv, s.nu, s.obs_dim, s.nparam
+        self.frame_skip, self.horizon = s.frame_skip, s.horizon
+        self.act_mid = self.model.arrays["task_act_mid"].astype(np.float32)
+        self.act_rng = self.model.arrays["task_act_rng"].astype(np.float32)
+        self.action_space = Box(-1.0, 1.0, (self.nu,))
+        self.observation_space = Box(-np.inf, np.inf, (self.obs_dim,))
+        self.obs = s.empty(num_envs, self.obs_dim)
+        self.reward = s.empty(num_envs)
+        self.done = s.empty(num_envs, dtype=torch.uint8)
+        self.goal = s.empty(num_envs, dtype=torch.uint8)
+        self.terminal_obs = s.empty(num_envs, self.obs_dim)
+        self._resets = 0
+
+    # --- episode control -------------------------------------------------------------------
+    def reset(self, mask=None, params=None, seed: Optional[int] = None):
+        """Reset all envs (or those with ``mask[i] != 0``); params [N, nparam] or sampled."""
+        if seed is None:
+            seed = self.seed + 7919 * self._resets
+        self._resets += 1
+        self.sim.reset(self.obs, params=params, mask=mask, seed=seed)
+        return self.obs
+
+    def step(self, actions):
+        """actions: device tensor [N, nu] in [-1, 1] (clipped and scaled in the kernel)."""
+        self.sim.step(actions, self.obs, self.reward, self.done, self.goal,
+                      terminal_obs=self.terminal_obs if self.autoreset else None,
+                      autoreset=self.autoreset, seed=self.seed)
+        terminated = (self.done & 1).bool()
+        truncated = (self.done & 2).bool()
+        info = {"goal_achieved": self.goal.bool(), "terminal_obs": self.terminal_obs}
+        return self.obs, self.reward, terminated, truncated, info
+
+    def random_actions(self, out, step: int, seed: int = 0):
+        self.sim.random_actions(out, seed, step)
+        return out
+
+    # --- state -----------------------------------------------------------------------------
+    def get_state(self) -> Dict[str, "object"]:
+        s = self.sim
+        st = dict(qpos=s.empty(self.num_envs, self.nq), qvel=s.empty(self.num_envs, self.nv),
+                  qacc_warmstart=s.empty(self.num_envs, self.nv), params=s.empty(self.num_envs, self.nparam))
+        s.get_state(st["qpos"], st["qvel"], st["qacc_warmstart"], st["params"])
+        return st
+
+    def set_state(self, qpos=None, qvel=None, qacc_warmstart=None, params=None):
+        self.sim.set_state(qpos, qvel, qacc_warmstart, params, obs=self.obs)
+        return self.obs
+
+    def episode_stats(self):
+        import torch
+        s = self.sim
+        out = dict(last_return=s.empty(self.num_envs), last_goal_steps=s.empty(self.num_envs, dtype=torch.int32),
+                   last_len=s.empty(self.num_envs, dtype=torch.int32),
+                   episodes=s.empty(self.num_envs, dtype=torch.int32))
+        s.episode_stats(out["last_return"], out["last_goal_steps"], out["last_len"], out["episodes"])
+        return out
+
+    def status(self):
+        import torch
+        out = self.sim.empty(self.num_envs, dtype=torch.int32)
+        self.sim.status(out)
+        return out
+
+    def evaluate_success(self, paths: List[dict]) -> float:
+        return _evaluate_success(self.env_id, paths)
+
+    def close(self):
+        self.sim.close()
+
+
+class _AdroitEnv:
+    """Single-env facade with the reference's method set (one ``AdroitVecEnv`` of size 1)."""
+
+    env_id: str = ""
+
+    def __init__(self, render_mode=None, width: int = 64, height: int = 64, is_headless: bool = True,
+                 variation_type: Optional[str] = None, device: int = 0, seed: Optional[int] = None):
+        import torch
+        self.render_mode, self.width, self.height = render_mode, width, height
+        self.is_headless = is_headless
+        self.variation_type = variation_type
+        self.vec = AdroitVecEnv(self.env_id, 1, device=device, variation_type=variation_type,
+                                seed=1, autoreset=False)
+        self.model = self.vec.model
+        self.frame_skip = self.vec.frame_skip
+        self.act_mid = self.vec.act_mid.astype(np.float64)
+        self.act_rng = self.vec.act_rng.astype(np.float64)
+        self.action_space = self.vec.action_space
+        self.observation_space = self.vec.observation_space
+        self._dev = self.vec.sim.torch_device
+        self._act = torch.zeros(1, self.vec.nu, device=self._dev)
+        self.np_random = np.random.default_rng(seed)
+        self._layout = param_layout(self.env_id, self.model, variation_type)
+        self._obs = np.zeros(self.vec.obs_dim, np.float32)
+        self.reset()
+
+    def seed(self, seed=None):
+        self.np_random = np.random.default_rng(seed)
+        return [seed]
+
+    # --- reference API ---------------------------------------------------------------------
+    def step(self, a):
+        import torch
+        a = np.asarray(a, np.float32).reshape(1, -1)
+        self._act.copy_(torch.from_numpy(a))
+        obs, rew, term, _trunc, info = self.vec.step(self._act)
+        self._obs = obs[0].cpu().numpy().copy()
+        return self._obs, float(rew[0]), bool(term[0]), {"goal_achieved": bool(info["goal_achieved"][0])}
+
+    def reset(self, seed=None):
+        if seed is not None:
+            self.seed(seed)
+        s = int(self.np_random.integers(1, 2 ** 63 - 1))
+        self.vec.reset(seed=s)
+        self._obs = self.vec.obs[0].cpu().numpy().copy()
+        return self._obs, {}
+
+    def reset_model(self):
+        return self.reset()
+
+    def get_obs(self):
+        return self._obs.copy()
+
+    def _params(self) -> np.ndarray:
+        return self.vec.get_state()["params"][0].cpu().numpy().astype(np.float64)
+
+    def _set(self, qpos, qvel, params):
+        import torch
+        t = lambda x: torch.as_tensor(np.asarray(x, np.float32).reshape(1, -1), device=self._dev)
+        self.vec.set_state(qpos=t(qpos), qvel=t(qvel), params=t(params))
+        self._obs = self.vec.obs[0].cpu().numpy().copy()
+
+    def _qpos_qvel(self):
+        st = self.vec.get_state()
+        return (st["qpos"][0].cpu().numpy().astype(np.float64), st["qvel"][0].cpu().numpy().astype(np.float64))
+
+    def evaluate_success(self, paths: List[dict]) -> float:
+        return _evaluate_success(self.env_id, paths)
+
+    def render(self, *args, **kwargs):
+        raise NotImplementedError("rendering is outside the accelerated path (see DESIGN.md, out of scope)")
+
+    def close(self):
+        self.vec.close()
+
+
+class HammerEnvV0(_AdroitEnv):
+    """``hand_manipulation_suite/hammer_v0.py`` (obs 46, frame_skip 5, horizon 200)."""
+    env_id = "hammer-v0"
+
+    def get_env_state(self):   # hammer_v0.py:134-143
+        qp, qv = self._qpos_qvel()
+        board = self.model.body_pos[self._layout[0][1]].astype(np.float64).copy()
+        board[2] = self._params()[0]
+        return dict(qpos=qp, qvel=qv, board_pos=board, target_pos=self._obs[42:45].astype(np.float64))
+
+    def set_env_state(self, state_dict):   # hammer_v0.py:145-153
+        p = self._params()
+        p[0] = np.asarray(state_dict["board_pos"])[2]
+        self._set(state_dict["qpos"], state_dict["qvel"], p)
+
+
+class DoorEnvV0(_AdroitEnv):
+    """``hand_manipulation_suite/door_v0.py`` (obs 39, frame_skip 1, horizon 200)."""
+    env_id = "door-v0"
+
+    def get_env_state(self):   # door_v0.py:121-128
+        qp, qv = self._qpos_qvel()
+        return dict(qpos=qp, qvel=qv, door_body_pos=self._params()[:3])
+
+    def set_env_state(self, state_dict):   # door_v0.py:130-138
+        self._set(state_dict["qpos"], state_dict["qvel"], np.asarray(state_dict["door_body_pos"])[:3])
+
+
+class PenEnvV0(_AdroitEnv):
+    """``hand_manipulation_suite/pen_v0.py`` (obs 45, frame_skip 5, horizon 100, done on drop)."""
+    env_id = "pen-v0"
+
+    def get_env_state(self):   # pen_v0.py:134-141
+        qp, qv = self._qpos_qvel()
+        return dict(qpos=qp, qvel=qv, desired_orien=self._params()[:4])
+
+    def set_env_state(self, state_dict):   # pen_v0.py:143-152
+        self._set(state_dict["qpos"], state_dict["qvel"], np.asarray(state_dict["desired_orien"])[:4])
+
+
+class RelocateEnvV0(_AdroitEnv):
+    """``hand_manipulation_suite/relocate_v0.py`` (obs 39, frame_skip 5, horizon 200).
+
+    ``get_env_state`` takes object / palm / target positions from a fresh forward pass of the
+    current state (the reference reads the previous forward's values; after ``reset`` or
+    ``set_env_state`` they coincide).  ``set_env_state`` writes the object's body x/y (the
+    reset-randomised components) and the target site position, as ``relocate_v0.py:118-129``.
+    """
+    env_id = "relocate-v0"
+
+    def get_env_state(self):   # relocate_v0.py:105-116
+        qp, qv = self._qpos_qvel()
+        d = self.vec.sim.forward_dump(0)
+        idx = self.model.arrays["task_idx"]
+        return dict(hand_qpos=qp[:30], obj_pos=d["xpos"][idx[1]].copy(), target_pos=d["site_xpos"][idx[2]].copy(),
+                    palm_pos=d["site_xpos"][idx[0]].copy(), qpos=qp, qvel=qv)
+
+    def set_env_state(self, state_dict):   # relocate_v0.py:118-129
+        obj = np.asarray(state_dict["obj_pos"])
+        tgt = np.asarray(state_dict["target_pos"])
+        self._set(state_dict["qpos"], state_dict["qvel"], np.array([obj[0], obj[1], tgt[0], tgt[1], tgt[2]]))

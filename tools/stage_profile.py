@@ -1,0 +1,80 @@
+"""Per-stage cycle breakdown of k_step (diagnostic build with -DAW_STAGE_PROF).
+
+    python tools/stage_profile.py --build          # here: compile mj_envs_amd/libadroit_hip_prof.so
+    python tools/stage_profile.py [--envs N] [--steps K] [--env hammer-v0]   # on the GPU box
+
+Cycles are s_memtime shader-clock ticks per wave, summed over waves; the report divides by
+the substep count to give cycles per wave-substep per stage.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF_LIB = os.path.join(REPO, "mj_envs_amd", "libadroit_hip_prof.so")
+
+
+def build(nv: int = 33):
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wno-unused-result", "-DAW_STAGE_PROF", f"-DAW_ONLY_NV={nv}", "-o", PROF_LIB,
+           os.path.join(REPO, "mj_envs_amd", "csrc", "adroit_wave.hip")]
+    subprocess.run(cmd, check=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--env", default="hammer-v0")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    if a.build:
+        build()
+        return
+    os.environ["AW_LIB"] = PROF_LIB
+    sys.path.insert(0, REPO)
+    import torch
+    from mj_envs_amd import _native
+    from mj_envs_amd.tasks import attach_task, load_model
+    m = attach_task(load_model(a.env), a.env)
+    sim = _native.Sim(m.to_blob(), a.envs)
+    obs = sim.empty(a.envs, sim.obs_dim)
+    act = sim.empty(a.envs, sim.nu)
+    rew, done, goal = sim.empty(a.envs), sim.empty(a.envs, dtype=torch.uint8), sim.empty(a.envs, dtype=torch.uint8)
+    sim.reset(obs, seed=1)
+    for k in range(5):
+        sim.random_actions(act, 0, k)
+        sim.step(act, obs, rew, done, goal, autoreset=True, seed=1)
+    torch.cuda.synchronize()
+    _native.stage_profile(reset=True)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for k in range(a.steps):
+        sim.random_actions(act, 0, 5 + k)
+        sim.step(act, obs, rew, done, goal, autoreset=True, seed=1)
+    ev[1].record()
+    torch.cuda.synchronize()
+    ms = ev[0].elapsed_time(ev[1]) / a.steps
+    p = _native.stage_profile(reset=True)
+    sub = max(1, p["substeps"])
+    names = _native.STAGES + _native.SUBSTAGES
+    tot = sum(p[k] for k in names)
+    rows = {k: dict(cycles_per_wave_substep=round(p[k] / sub, 1), frac=round(p[k] / max(tot, 1), 4))
+            for k in names}
+    res = dict(env=a.env, envs=a.envs, steps=a.steps, ms_per_step=round(ms, 3), waves=p["waves"],
+               substeps=p["substeps"], cycles_per_wave_substep=round(tot / sub, 1), stages=rows,
+               avg_newton_iters_per_solve=round(p["newton_iters"] / sub, 3),
+               avg_noslip_iters_per_substep=round(p["noslip_iters"] / sub, 3),
+               avg_nefc=round(p["nefc"] / sub, 3), avg_ncon=round(p["ncon"] / sub, 3))
+    txt = json.dumps(res, indent=1)
+    print(txt)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(txt)
+
+
+if __name__ == "__main__":
+    main()
