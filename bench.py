@@ -78,11 +78,11 @@ def main():
     import torch
     import torch.distributed as dist
     from mj_envs_amd import _native, perfmodel
+    from mj_envs_amd.dist import EpisodeGather, rank_seed, shard_from_env
     from mj_envs_amd.tasks import attach_task, load_model
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    shard = shard_from_env(args.envs_per_gpu)
+    world, rank, local = shard.world, shard.rank, shard.local_rank
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -101,9 +101,8 @@ def main():
     goal = sim.empty(n, dtype=torch.uint8)
     last_ret = sim.empty(n)
     last_goal = sim.empty(n, dtype=torch.int32)
-    gathered_ret = sim.empty(world * n)
-    gathered_goal = sim.empty(world * n, dtype=torch.int32)
-    seed = 1 + rank                          # per-rank Philox key: global env id = (rank, env)
+    gather = EpisodeGather(n, world, dev)
+    seed = rank_seed(1, rank)                # per-rank Philox key: global env id = (rank, env)
     sim.reset(obs, seed=seed)
 
     def one_step(k, ev=None):
@@ -115,9 +114,7 @@ def main():
             ev[1].record()
         if (k + 1) % sim.horizon == 0:       # every env finished an episode this step
             sim.episode_stats(last_ret, last_goal)
-            if world > 1:
-                dist.all_gather_into_tensor(gathered_ret, last_ret)
-                dist.all_gather_into_tensor(gathered_goal, last_goal)
+            gather(last_ret, last_goal)      # RCCL all-gather over xGMI when world > 1
 
     for k in range(args.warmup):
         one_step(k)

@@ -167,6 +167,10 @@ class _AdroitEnv:
         self.np_random = np.random.default_rng(seed)
         return [seed]
 
+    @property
+    def unwrapped(self):
+        return self
+
     # --- reference API ---------------------------------------------------------------------
     def step(self, a):
         import torch
