@@ -34,53 +34,88 @@ struct DState {
 };
 
 // ---------------------------------------------------------------------------------------
-// contacts -> key order (bitonic sort of (key, slot) over the wave), then frames
+// contacts -> (pair, emission) key order: rank of each key among the n keys (keys are unique),
+// then a scatter to that slot; frames are completed on the way
 AW_DEV void sort_contacts(Env& s, int lane) {
   int n = s.ncon;
   if (n > MAXCON) n = MAXCON;
-  int key = lane < n ? s.con_key[lane] : 0x7fffffff;
-  int idx = lane;
-#pragma unroll
-  for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      int pk = __shfl_xor(key, j, 64), pi = __shfl_xor(idx, j, 64);
-      bool up = (lane & k) == 0;
-      bool lower = (lane & j) == 0;
-      bool take = (lower == up) ? (pk < key) : (pk > key);
-      if (take) { key = pk; idx = pi; }
-    }
-  }
+  const int key = lane < n ? s.con_key[lane] : 0x7fffffff;
+  int rank = 0;
+  for (int j = 0; j < n; j++) rank += rlane_i(key, j) < key ? 1 : 0;
   float dist = 0.f, pos[3] = {0, 0, 0}, nrm[3] = {0, 0, 0};
   int pair = 0;
   if (lane < n) {
-    dist = s.con_dist[idx];
-    pair = s.con_pair[idx];
-    for (int k = 0; k < 3; k++) { pos[k] = s.con_pos[idx][k]; nrm[k] = s.con_frame[idx][k]; }
+    dist = s.con_dist[lane];
+    pair = s.con_pair[lane];
+    for (int k = 0; k < 3; k++) { pos[k] = s.con_pos[lane][k]; nrm[k] = s.con_frame[lane][k]; }
   }
   wsync();
   if (lane < n) {
-    s.con_key[lane] = key;
-    s.con_dist[lane] = dist;
-    s.con_pair[lane] = pair;
-    copy3(s.con_pos[lane], pos);
+    s.con_key[rank] = key;
+    s.con_dist[rank] = dist;
+    s.con_pair[rank] = pair;
+    copy3(s.con_pos[rank], pos);
     float f[9] = {nrm[0], nrm[1], nrm[2], 0, 0, 0, 0, 0, 0};
     make_frame(f);
-    for (int k = 0; k < 9; k++) s.con_frame[lane][k] = f[k];
+    for (int k = 0; k < 9; k++) s.con_frame[rank][k] = f[k];
   }
   if (lane == 0) s.ncon = n;
   wsync();
 }
 
+// mj_collision: bounding-sphere broadphase over the static candidate list (one pair per lane,
+// 64 per round), survivors compacted class-major into an LDS list (ballot + mbcnt), then ONE
+// narrowphase loop over the list: lanes of a round mostly share a collider, instead of every
+// round executing every collider branch its lanes happen to need.
 AW_DEV void stage_collision(const DModel& m, Env& s, int lane) {
   if (lane == 0) s.ncon = 0;
   wsync();
-  if (!(m.disableflags & (DSBL_CONSTRAINT | DSBL_CONTACT)))
-    {
-#ifndef X_NOCOLL
-    for (int p = lane; p < m.npairall; p += 64) collide_pair(m, s, p);
-#endif
+  if (!(m.disableflags & (DSBL_CONSTRAINT | DSBL_CONTACT))) {
+    short* plist = reinterpret_cast<short*>(&s.J[0][0]);   // dense J rows are dead until stage_constraints
+    int cnt[NCLASS];
+#pragma unroll
+    for (int c = 0; c < NCLASS; c++) cnt[c] = 0;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    for (int base = 0; base < m.npairall; base += 64) {
+      const int p = base + lane;
+      bool pass = false;
+      int cls = -1;
+      if (p < m.npairall) {
+        cls = m.cp_class[p];
+        const float rb = m.cp_rb[p];
+        if (rb < 0.f) {
+          pass = true;
+        } else {
+          const int g1 = m.cp_g1[p], g2 = m.cp_g2[p];
+          float dif[3];
+          sub3(dif, s.gxpos[g1], s.gxpos[g2]);
+          pass = !(norm3(dif) > rb);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < NCLASS; c++) {
+        const bool mine = pass && cls == c;
+        const unsigned long long mask = __ballot(mine);
+        if (mine) plist[m.cls_start[c] + cnt[c] + __popcll(mask & below)] = (short)p;
+        cnt[c] += __popcll(mask);
+      }
     }
+    int pre[NCLASS + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int c = 0; c < NCLASS; c++) pre[c + 1] = pre[c] + cnt[c];
+    wsync();
+    for (int i = lane; i < pre[NCLASS]; i += 64) {
+      int c = 0;
+#pragma unroll
+      for (int k = 1; k < NCLASS; k++) c += i >= pre[k] ? 1 : 0;
+      int off = i, st = 0;
+#pragma unroll
+      for (int k = 0; k < NCLASS; k++)
+        if (k == c) { off = i - pre[k]; st = m.cls_start[k]; }
+      collide_pair(m, s, plist[st + off]);
+    }
+  }
   wsync();
   sort_contacts(s, lane);
 }
@@ -686,6 +721,30 @@ static int build_model(const Blob& B, DModel& m, Packer& P) {
     }
   }
   m.npairall = (int)pg1.size();
+  {
+    // collider class per pair (aw_collide.h collide_pair dispatch) and the broadphase radius
+    std::vector<int> pcls(m.npairall);
+    std::vector<float> prb(m.npairall);
+    int ccount[NCLASS] = {0, 0, 0, 0, 0};
+    for (int p = 0; p < m.npairall; p++) {
+      int a = pg1[p], b = pg2[p];
+      int ta = ctype[a], tb = ctype[b];
+      int lo = std::min(ta, tb), hi = std::max(ta, tb);
+      int c;
+      if (lo == GEOM_PLANE) c = 0;
+      else if (lo == GEOM_CYLINDER || hi == GEOM_CYLINDER) c = 4;
+      else if (hi == GEOM_BOX && lo == GEOM_BOX) c = 3;
+      else if (hi == GEOM_BOX) c = 2;
+      else c = 1;
+      pcls[p] = c;
+      ccount[c]++;
+      prb[p] = lo == GEOM_PLANE ? -1.f : (float)((double)crb[a] + (double)crb[b] + (double)pmg[p]);
+    }
+    m.cls_start[0] = 0;
+    for (int c = 0; c < NCLASS; c++) m.cls_start[c + 1] = m.cls_start[c] + ccount[c];
+    if (m.npairall > MAXDENSE * VS * 2) return fail(AW_EUNSUPPORTED, "too many collision pairs");
+    P.add(&m.cp_class, pcls); P.add(&m.cp_rb, prb);
+  }
   P.add(&m.cp_g1, pg1); P.add(&m.cp_g2, pg2); P.add(&m.cp_condim, pcd); P.add(&m.cp_friction, pfr);
   P.add(&m.cp_solref, psr); P.add(&m.cp_solimp, psi); P.add(&m.cp_margin, pmg); P.add(&m.cp_gap, pgp);
 

@@ -718,12 +718,7 @@ AW_DEV void collide_pair(const DModel& m, Env& s, int pair) {
     a.pos[k] = s.gxpos[g1][k]; b.pos[k] = s.gxpos[g2][k];
     a.size[k] = s.gsize[g1][k]; b.size[k] = s.gsize[g2][k];
   }
-  float margin = m.cp_margin[pair];
-  if (a.type != GEOM_PLANE && b.type != GEOM_PLANE) {
-    float dif[3];
-    sub3(dif, a.pos, b.pos);
-    if (norm3(dif) > m.geom_rbound[g1] + m.geom_rbound[g2] + margin) return;
-  }
+  float margin = m.cp_margin[pair];   // the bounding-sphere test ran in the broadphase
   for (int k = 0; k < 9; k++) { a.mat[k] = s.gxmat[g1][k]; b.mat[k] = s.gxmat[g2][k]; }
   Emit e{&s, pair, 0};
   // every non-plane pair with a cylinder goes through MPR (mjc_Convex); one inlined call site

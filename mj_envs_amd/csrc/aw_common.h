@@ -28,6 +28,7 @@ constexpr int MAXP = 8;       // per-env model parameters
 constexpr int MAXLEV = 16;    // kinematic tree depth
 constexpr int MAXTOUCH = 4;   // task touch sensors
 constexpr int MAXPAIRCON = 8; // contacts per geom pair
+constexpr int NCLASS = 5;      // collider classes: plane-*, round-round, round-box, box-box, MPR
 
 constexpr float MINVAL = 1e-15f;
 
@@ -128,6 +129,10 @@ struct DModel {
   const int* cp_g1; const int* cp_g2; const int* cp_condim;
   const float* cp_friction; const float* cp_solref; const float* cp_solimp; const float* cp_margin;
   const float* cp_gap;
+  // broadphase: collider class of each pair (narrowphase is run class-major after compaction),
+  // bounding-sphere radius sum rbound1 + rbound2 + margin (< 0: plane pair, always tested)
+  const int* cp_class; const float* cp_rb;
+  int cls_start[NCLASS + 1];  // class c owns list slots [cls_start[c], cls_start[c+1])
 
   const int* task_idx; const int* param_field; const int* param_obj; const int* param_comp;
   const float* act_mid; const float* act_rng; const float* param_default;

@@ -311,6 +311,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
 // ---------------------------------------------------------------------------------------
 // Newton solver
 constexpr float GRAD_NOISE = 2e-6f;   // ~16 fp32 ulps of the gradient's terms
+constexpr int NSP_CACHE = 8;          // noslip edge pairs whose J / X rows stay in VGPRs
 struct RowR {
   float D, floss, Jaref, Jp, force;
   int st, fr, valid;
@@ -577,6 +578,41 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
   wsync();
   qacc = lane < NV ? qacc : 0.f;
   const float scale = 1.f / (m.meaninertia * (float)(NV > 1 ? NV : 1));
+  // compact list of active edge pairs (K >= MINVAL), pair p's constants in lane p; the J / X
+  // rows of the first NSP_CACHE pairs are cached in VGPRs for the sweeps
+  int npr, pr_e = 0;
+  float pr_a11 = 0.f, pr_a22 = 0.f, pr_a12 = 0.f, pr_ik = 0.f, pr_ar1 = 0.f, pr_ar2 = 0.f;
+  {
+    int* lst = reinterpret_cast<int*>(s.rowbuf);   // rowbuf is dead between Newton and jt_mul
+    const int e = lane;
+    bool act = false;
+    if (e + 1 < ndense && s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1) {
+      const float K = s.ns_a[e][0] + s.ns_a[e][1] - 2.f * s.ns_a[e][2];
+      act = K >= MINVAL;
+    }
+    const unsigned long long msk = __ballot(act);
+    if (act) lst[__popcll(msk & ((1ull << lane) - 1ull))] = e;
+    npr = __popcll(msk);
+    wsync();
+    if (lane < npr) {
+      pr_e = lst[lane];
+      pr_a11 = s.ns_a[pr_e][0]; pr_a22 = s.ns_a[pr_e][1]; pr_a12 = s.ns_a[pr_e][2];
+      pr_ik = 1.0f / (pr_a11 + pr_a22 - 2.f * pr_a12);
+      pr_ar1 = s.efc_aref[nsparse + pr_e];
+      pr_ar2 = s.efc_aref[nsparse + pr_e + 1];
+    }
+    wsync();
+  }
+  float c_j1[NSP_CACHE], c_j2[NSP_CACHE], c_x1[NSP_CACHE], c_x2[NSP_CACHE];
+#pragma unroll
+  for (int p = 0; p < NSP_CACHE; p++) {
+    c_j1[p] = c_j2[p] = c_x1[p] = c_x2[p] = 0.f;
+    if (p < npr) {
+      const int e = rlane_i(pr_e, p);
+      c_j1[p] = lm * s.J[e][li]; c_j2[p] = lm * s.J[e + 1][li];
+      c_x1[p] = lm * s.X[e][li]; c_x2[p] = lm * s.X[e + 1][li];
+    }
+  }
   AW_PROF(s, PR_NS_SETUP);
   if (lane == 0) s.it_noslip = 0;
   for (int it = 0; it < m.noslip_iterations; it++) {
@@ -600,23 +636,27 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
       qacc = fmaf(Mi[d], delta, qacc);
     }
     impr -= wave_sum(imp_l);
-    for (int e = 0; e + 1 < ndense; e++) {
-      if (!(s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1)) continue;
-      float A11 = s.ns_a[e][0], A22 = s.ns_a[e][1], A12 = s.ns_a[e][2];
-      float K = A11 + A22 - 2.f * A12;
-      if (K < MINVAL) continue;
-      float x1 = lm * s.X[e][li], x2 = lm * s.X[e + 1][li];
-      float r1 = wave_sum(lm * s.J[e][li] * qacc) - s.efc_aref[nsparse + e];
-      float r2 = wave_sum(lm * s.J[e + 1][li] * qacc) - s.efc_aref[nsparse + e + 1];
-      float f1 = rlane(fd, e), f2 = rlane(fd, e + 1);
-      float sum = f1 + f2, x = f1 - f2;
-      float xn = clampf(x - 2.f * (r1 - r2) / K, -sum, sum);
-      float d1 = 0.5f * (sum + xn) - f1, d2 = 0.5f * (sum - xn) - f2;
-      if (d1 == 0.f && d2 == 0.f) continue;
+    // opposing pyramid-edge pairs, in row order (branch-free: a zero update is an exact no-op)
+    auto pair_step = [&](int p, float j1, float j2, float x1, float x2) {
+      const int e = rlane_i(pr_e, p);
+      const float A11 = rlane(pr_a11, p), A22 = rlane(pr_a22, p), A12 = rlane(pr_a12, p);
+      const float r1 = wave_sum(j1 * qacc) - rlane(pr_ar1, p);
+      const float r2 = wave_sum(j2 * qacc) - rlane(pr_ar2, p);
+      const float f1 = rlane(fd, e), f2 = rlane(fd, e + 1);
+      const float sum = f1 + f2, x = f1 - f2;
+      const float xn = clampf(x - 2.f * (r1 - r2) * rlane(pr_ik, p), -sum, sum);
+      const float d1 = 0.5f * (sum + xn) - f1, d2 = 0.5f * (sum - xn) - f2;
       impr -= r1 * d1 + r2 * d2 + 0.5f * (A11 * d1 * d1 + 2.f * A12 * d1 * d2 + A22 * d2 * d2);
       qacc = fmaf(x1, d1, fmaf(x2, d2, qacc));
       if (lane == e) fd = f1 + d1;
       if (lane == e + 1) fd = f2 + d2;
+    };
+#pragma unroll
+    for (int p = 0; p < NSP_CACHE; p++)
+      if (p < npr) pair_step(p, c_j1[p], c_j2[p], c_x1[p], c_x2[p]);
+    for (int p = NSP_CACHE; p < npr; p++) {
+      const int e = rlane_i(pr_e, p);
+      pair_step(p, lm * s.J[e][li], lm * s.J[e + 1][li], lm * s.X[e][li], lm * s.X[e + 1][li]);
     }
     if (impr * scale < m.noslip_tolerance) break;
   }
