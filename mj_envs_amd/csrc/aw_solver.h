@@ -27,9 +27,9 @@ AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
   float* col = reinterpret_cast<float*>(s.colbuf);
 #pragma unroll
   for (int j = 0; j < NV; j++) {
-    const float djj = rlane(row[j], j);
-    const float sq = sqrtf(fmaxf(djj, MINVAL));
-    const float inv = 1.0f / sq;
+    const float djj = fmaxf(rlane(row[j], j), MINVAL);
+    const float inv = __builtin_amdgcn_rsqf(djj);   // v_rsq_f32: one op on the column's critical path
+    const float sq = djj * inv;
     row[j] = lane == j ? sq : row[j] * inv;
     if (lane == j) invd = inv;
     if (j + 1 < NV) {

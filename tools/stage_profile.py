@@ -17,8 +17,9 @@ PROF_LIB = os.path.join(REPO, "mj_envs_amd", "libadroit_hip_prof.so")
 
 
 def build(nv: int = 33):
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", "-DAW_STAGE_PROF", f"-DAW_ONLY_NV={nv}", "-o", PROF_LIB,
+    sys.path.insert(0, REPO)
+    from __graft_entry__ import HIPCC_FLAGS
+    cmd = ["/opt/rocm/bin/hipcc", *HIPCC_FLAGS, "-DAW_STAGE_PROF", f"-DAW_ONLY_NV={nv}", "-o", PROF_LIB,
            os.path.join(REPO, "mj_envs_amd", "csrc", "adroit_wave.hip")]
     subprocess.run(cmd, check=True)
 
