@@ -52,9 +52,11 @@ def cpu_baseline(model_blob, env_id, budget_s=12.0):
 
 def pmc_traffic(env_per_launch):
     """HBM bytes per k_step launch from the committed rocprofv3 --pmc summary, or None."""
-    path = os.path.join(REPO, "profiles", "r01_pmc_kstep.json")
-    if not os.path.exists(path):
+    import glob
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_kstep.json")))
+    if not paths:
         return None
+    path = paths[-1]                         # latest round's counters
     try:
         with open(path) as f:
             d = json.load(f)

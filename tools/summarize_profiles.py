@@ -1,0 +1,74 @@
+"""Copy the judged parts of a gpurun_out/<tag> pass (tools/gpu_round.sh) into profiles/.
+
+    python tools/summarize_profiles.py r01
+
+Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats summary),
+profiles/<tag>_pmc_kstep.json (FETCH_SIZE / WRITE_SIZE of every k_step launch, per launch),
+profiles/<tag>_bench.json (the bench line of the same pass) and profiles/<tag>_pytest_gpu.txt.
+"""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def pmc(path, counter, kernel="k_step"):
+    vals, meta = [], {}
+    for r in csv.DictReader(open(path)):
+        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            vals.append(float(r["Counter_Value"]))
+            meta = dict(grid=int(r["Grid_Size"]), wg=int(r["Workgroup_Size"]), lds=int(r["LDS_Block_Size"]),
+                        scratch=int(r["Scratch_Size"]), vgpr=int(r["VGPR_Count"]), sgpr=int(r["SGPR_Count"]),
+                        name=r["Kernel_Name"])
+    return vals, meta
+
+
+def main(tag):
+    src = os.path.join(REPO, "gpurun_out", tag)
+    dst = os.path.join(REPO, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "kt_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    bench = open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1]
+    b = json.loads(bench)
+    with open(os.path.join(dst, f"{tag}_bench.json"), "w") as f:
+        f.write(bench + "\n")
+    log = os.path.join(src, "pytest_gpu.log")
+    if os.path.exists(log):
+        shutil.copy(log, os.path.join(dst, f"{tag}_pytest_gpu.txt"))
+    fetch, meta = pmc(os.path.join(src, "pmc_fetch", "pf_counter_collection.csv"), "FETCH_SIZE")
+    write, _ = pmc(os.path.join(src, "pmc_write", "pw_counter_collection.csv"), "WRITE_SIZE")
+    # calibration kernel on the same box: k_random_actions writes exactly n*nu*4 bytes
+    cal, _ = pmc(os.path.join(src, "pmc_write", "pw_counter_collection.csv"), "WRITE_SIZE", "k_random_actions")
+    envs = meta["grid"] // meta["wg"]
+    fetch_b = statistics.mean(fetch) * 1024
+    write_b = statistics.mean(write) * 1024
+    nu = 26 if "hammer" in b["config"]["workload"] else None
+    out = dict(
+        tag=tag, kernel=meta["name"], envs=envs, launches=len(fetch),
+        fetch_size_kb=[round(v, 3) for v in fetch], write_size_kb=[round(v, 3) for v in write],
+        fetch_bytes_per_launch=round(fetch_b), write_bytes_per_launch=round(write_b),
+        hbm_bytes_per_launch=round(fetch_b + write_b),
+        hbm_bytes_per_env_step=round((fetch_b + write_b) / envs, 1),
+        algorithmic_bytes_per_env_step=b["roofline"]["bytes_per_env_step"],
+        write_calibration=None if not cal or nu is None else dict(
+            kernel="k_random_actions", exact_bytes=envs * nu * 4,
+            write_size_bytes=round(statistics.mean(cal) * 1024),
+            ratio=round(statistics.mean(cal) * 1024 / (envs * nu * 4), 3)),
+        kernel_resources=dict((k, meta[k]) for k in ("wg", "lds", "scratch", "vgpr", "sgpr")),
+        method="rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
+               "`python bench.py --steps 3 --warmup 1 --no-cpu-baseline` (MI355X_MICROARCH.md HBM section); "
+               "counters are KB (x1024). FETCH_SIZE is NOT doubled: the 1/2 tally the guide documents is for "
+               "16 B/lane streaming reads, while k_step reads each env's state as one 4 B/lane row per wave "
+               "(uncalibrated width); raw counter bytes are reported.")
+    with open(os.path.join(dst, f"{tag}_pmc_kstep.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps({k: out[k] for k in ("envs", "hbm_bytes_per_launch", "hbm_bytes_per_env_step",
+                                          "algorithmic_bytes_per_env_step", "write_calibration")}))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
