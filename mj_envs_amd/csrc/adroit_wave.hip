@@ -21,6 +21,10 @@
 
 using namespace aw;
 
+#ifndef AW_KSTEP_ATTR
+#define AW_KSTEP_ATTR
+#endif
+
 #ifdef AW_STAGE_PROF
 __device__ unsigned long long g_stage_prof[AW_NPROF];
 #endif
@@ -298,7 +302,7 @@ AW_DEV void reset_env(const DModel& m, Env& s, const DState& st, int env, int la
 // substeps, the mj_checkAcc retry and the reset forward through it), which keeps the code
 // object small enough for the instruction cache.
 template <int NV>
-__global__ void __launch_bounds__(64) k_step(DModel m, DState st, int n, const float* __restrict__ actions,
+__global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel m, DState st, int n, const float* __restrict__ actions,
                                              float* obs, float* reward, uint8_t* done, uint8_t* goal,
                                              float* terminal_obs, int autoreset, uint64_t seed) {
   __shared__ Env s;
