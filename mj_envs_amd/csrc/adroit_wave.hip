@@ -21,8 +21,10 @@
 
 using namespace aw;
 
+// k_step is allocated for two waves per SIMD (<= 256 VGPRs): its LDS footprint (< 20 KiB)
+// already admits 8 envs per CU, and the register allocator left alone would take 350+
 #ifndef AW_KSTEP_ATTR
-#define AW_KSTEP_ATTR
+#define AW_KSTEP_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
 #endif
 
 #ifdef AW_STAGE_PROF
@@ -39,7 +41,7 @@ struct DState {
 
 // ---------------------------------------------------------------------------------------
 // contacts -> (pair, emission) key order: rank of each key among the n keys (keys are unique),
-// then a scatter to that slot; frames are completed on the way
+// then a scatter to that slot; normals are normalised on the way
 AW_DEV void sort_contacts(Env& s, int lane) {
   int n = s.ncon;
   if (n > MAXCON) n = MAXCON;
@@ -51,7 +53,7 @@ AW_DEV void sort_contacts(Env& s, int lane) {
   if (lane < n) {
     dist = s.con_dist[lane];
     pair = s.con_pair[lane];
-    for (int k = 0; k < 3; k++) { pos[k] = s.con_pos[lane][k]; nrm[k] = s.con_frame[lane][k]; }
+    for (int k = 0; k < 3; k++) { pos[k] = s.con_pos[lane][k]; nrm[k] = s.con_nrm[lane][k]; }
   }
   wsync();
   if (lane < n) {
@@ -59,9 +61,8 @@ AW_DEV void sort_contacts(Env& s, int lane) {
     s.con_dist[rank] = dist;
     s.con_pair[rank] = pair;
     copy3(s.con_pos[rank], pos);
-    float f[9] = {nrm[0], nrm[1], nrm[2], 0, 0, 0, 0, 0, 0};
-    make_frame(f);
-    for (int k = 0; k < 9; k++) s.con_frame[rank][k] = f[k];
+    normalize3(nrm);              // mju_makeFrame's first step; tangents are rebuilt where used
+    copy3(s.con_nrm[rank], nrm);
   }
   if (lane == 0) s.ncon = n;
   wsync();
@@ -124,17 +125,28 @@ AW_DEV void stage_collision(const DModel& m, Env& s, int lane) {
   sort_contacts(s, lane);
 }
 
-// mj_forward: everything up to qacc / forces / sensors; Mrow is left in registers
+// lane-local dof vectors of a forward pass (VGPRs; lane = dof)
+struct Dof {
+  float qacc, qacc_smooth, qfrc_smooth, qfrc_con;
+};
+
+// mj_forward: everything up to qacc / forces / sensors; Mrow is left in registers.  Stage order
+// follows the LDS overlays (aw_common.h Env): the constraint rows are assembled while the
+// phase-K arrays (cdof, subcom) are alive, then the solver phase reuses that storage.
 template <int NV>
-AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
+AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV], Dof& d) {
   stage_kinematics(m, s, lane);
   AW_PROF(s, PR_KIN);
   stage_collision(m, s, lane);
   AW_PROF(s, PR_COLL);
   stage_com(m, s, lane);
+  d.qfrc_smooth = stage_velocity(m, s, lane);
+  AW_PROF(s, PR_SMOOTH);
   stage_crb<NV>(m, s, lane, Mrow);
   AW_PROF(s, PR_CRB);
-  stage_velocity(m, s, lane);
+  if (lane == 0) { s.it_newton = 0; s.it_noslip = 0; }
+  stage_constraints<NV>(m, s, lane);
+  AW_PROF(s, PR_CONSTR);
   // qacc_smooth = M \ qfrc_smooth
   {
     float row[NV];
@@ -144,34 +156,23 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
     chol_factor<NV>(row, lane, invd, s);
     chol_store<NV>(row, lane, s);
     wsync();
-    float fs = lane < NV ? s.qfrc_smooth[lane] : 0.f;
-    float x = chol_solve<NV>(row, invd, fs, lane, s);
-    if (lane < NV) s.qacc_smooth[lane] = x;
-    wsync();
+    d.qacc_smooth = chol_solve<NV>(row, invd, lane < NV ? d.qfrc_smooth : 0.f, lane, s);
   }
   AW_PROF(s, PR_SMOOTH);
-  if (lane == 0) { s.it_newton = 0; s.it_noslip = 0; }
-  stage_constraints<NV>(m, s, lane);
-  AW_PROF(s, PR_CONSTR);
   if (s.nefc == 0) {
-    if (lane < NV) { s.qacc[lane] = s.qacc_smooth[lane]; s.qfrc_con[lane] = 0.f; }
-    wsync();
+    d.qacc = d.qacc_smooth;
+    d.qfrc_con = 0.f;
   } else {
     float a = 0.f;
-#ifndef X_NONEWTON
-    solve_newton<NV>(m, s, lane, Mrow, a);
+    solve_newton<NV>(m, s, lane, Mrow, a, d.qfrc_smooth, d.qacc_smooth);
     AW_PROF(s, PR_NEWTON);
-#endif
-    
-#ifndef X_NONOSLIP
     if (m.noslip_iterations > 0 && !(m.disableflags & DSBL_NOSLIP)) solve_noslip<NV>(m, s, lane, Mrow, a);
     AW_PROF(s, PR_NOSLIP);
-#endif
     for (int r = lane; r < s.nefc; r += 64) s.rowbuf[r] = s.efc_force[r];
     wsync();
     float qc = jt_mul<NV>(s, lane);
-    if (lane < NV) { s.qacc[lane] = a; s.qfrc_con[lane] = qc; }
-    wsync();
+    d.qacc = lane < NV ? a : 0.f;
+    d.qfrc_con = lane < NV ? qc : 0.f;
   }
   stage_touch(m, s, lane);
   AW_PROF(s, PR_JT_TOUCH);
@@ -179,7 +180,7 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
 
 // mj_Euler: implicit joint damping, semi-implicit positions, warmstart <- qacc
 template <int NV>
-AW_DEV void euler(const DModel& m, Env& s, int lane, const float (&Mrow)[NV]) {
+AW_DEV void euler(const DModel& m, Env& s, int lane, const float (&Mrow)[NV], const Dof& d) {
   const float h = m.timestep;
   const bool dmp = !(m.disableflags & (DSBL_EULERDAMP | DSBL_PASSIVE));
   float acc;
@@ -192,16 +193,16 @@ AW_DEV void euler(const DModel& m, Env& s, int lane, const float (&Mrow)[NV]) {
     chol_factor<NV>(row, lane, invd, s);
     chol_store<NV>(row, lane, s);
     wsync();
-    float f = lane < NV ? s.qfrc_smooth[lane] + s.qfrc_con[lane] : 0.f;
+    float f = lane < NV ? d.qfrc_smooth + d.qfrc_con : 0.f;
     acc = chol_solve<NV>(row, invd, f, lane, s);
   } else {
-    acc = lane < NV ? s.qacc[lane] : 0.f;
+    acc = d.qacc;
   }
   if (lane < NV) {
     float v = s.qvel[lane] + h * acc;
     s.qvel[lane] = v;
     s.qpos[lane] += h * v;
-    s.warm[lane] = s.qacc[lane];
+    s.warm[lane] = d.qacc;
   }
   wsync();
 }
@@ -227,8 +228,8 @@ AW_DEV void check_state(Env& s, int lane) {
 }
 // mj_checkAcc: bad qacc -> flag + reset; the caller re-runs forward
 template <int NV>
-AW_DEV bool check_acc(Env& s, int lane) {
-  if (__ballot(lane < NV && bad_value(s.qacc[lane]))) {
+AW_DEV bool check_acc(Env& s, int lane, const Dof& d) {
+  if (__ballot(lane < NV && bad_value(d.qacc))) {
     if (lane == 0) s.status |= ST_BADQACC;
     reset_state<NV>(s, lane);
     return true;
@@ -293,7 +294,8 @@ AW_DEV void reset_env(const DModel& m, Env& s, const DState& st, int env, int la
                       const float* params_in, uint64_t seed, float* obs) {
   reset_prepare<NV>(m, s, st, env, lane, params_in, seed);
   float Mrow[NV];
-  forward<NV>(m, s, lane, Mrow);
+  Dof d;
+  forward<NV>(m, s, lane, Mrow, d);
   if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
 }
 
@@ -316,19 +318,23 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel m, DState st, 
   }
   stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
   float Mrow[NV];
+  Dof d;
   float* ob = obs + (size_t)env * m.obs_dim;
   int sub = 0;
   bool resetting = false, retry = false;
   AW_PROF(s, PR_PRE);
 #pragma nounroll
   while (true) {
+    // memory clobber: keeps LICM from hoisting the (loop-invariant) model loads of a whole
+    // substep out of this loop, which would pin them in registers across every stage
+    asm volatile("" ::: "memory");
     if (!resetting && !retry) check_state<NV>(s, lane);
     AW_PROF(s, PR_CHECK);
-    forward<NV>(m, s, lane, Mrow);
+    forward<NV>(m, s, lane, Mrow, d);
     if (resetting) break;
-    if (!retry && check_acc<NV>(s, lane)) { retry = true; continue; }
+    if (!retry && check_acc<NV>(s, lane, d)) { retry = true; continue; }
     retry = false;
-    euler<NV>(m, s, lane, Mrow);
+    euler<NV>(m, s, lane, Mrow, d);
     AW_PROF(s, PR_EULER);
     AW_PROF_COUNT(s, PR_SUBSTEPS);
     if (++sub < m.frame_skip) continue;
@@ -413,7 +419,8 @@ __global__ void __launch_bounds__(64) k_set_state(DModel m, DState st, int n, co
   if (lane < m.nu) s.ctrl[lane] = 0.f;
   stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
   float Mrow[NV];
-  forward<NV>(m, s, lane, Mrow);
+  Dof d;
+  forward<NV>(m, s, lane, Mrow, d);
   if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
   store_env<NV>(m, s, st, env, lane);
 }
@@ -427,16 +434,17 @@ __global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const
   if (lane < m.nu) s.ctrl[lane] = ctrl ? ctrl[lane] : 0.f;
   stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
   float Mrow[NV];
-  forward<NV>(m, s, lane, Mrow);
+  Dof d;
+  forward<NV>(m, s, lane, Mrow, d);
   for (int i = lane; i < MAXB * 3; i += 64) out[i] = i < m.nbody * 3 ? (&s.xpos[0][0])[i] : 0.f;
   for (int i = lane; i < MAXB * 4; i += 64) out[96 + i] = i < m.nbody * 4 ? (&s.xquat[0][0])[i] : 0.f;
   for (int i = lane; i < MAXS * 3; i += 64) out[224 + i] = i < m.nsite * 3 ? (&s.sxpos[0][0])[i] : 0.f;
   if (lane < MAXV) {
     bool v = lane < NV;
-    out[320 + lane] = v ? s.qacc_smooth[lane] : 0.f;
-    out[356 + lane] = v ? s.qfrc_smooth[lane] : 0.f;
-    out[392 + lane] = v ? s.qacc[lane] : 0.f;
-    out[428 + lane] = v ? s.qfrc_con[lane] : 0.f;
+    out[320 + lane] = v ? d.qacc_smooth : 0.f;
+    out[356 + lane] = v ? d.qfrc_smooth : 0.f;
+    out[392 + lane] = v ? d.qacc : 0.f;
+    out[428 + lane] = v ? d.qfrc_con : 0.f;
   }
   for (int k = 0; k < NV; k++)
     if (lane < NV) out[464 + lane * NV + k] = Mrow[k];
@@ -449,7 +457,10 @@ __global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const
     bool v = lane < s.ncon;
     out[1768 + lane] = v ? s.con_dist[lane] : 0.f;
     for (int k = 0; k < 3; k++) out[1800 + 3 * lane + k] = v ? s.con_pos[lane][k] : 0.f;
-    for (int k = 0; k < 9; k++) out[1896 + 9 * lane + k] = v ? s.con_frame[lane][k] : 0.f;
+    float fr[9];
+    for (int k = 0; k < 3; k++) { fr[k] = v ? s.con_nrm[lane][k] : 1.f; fr[3 + k] = 0.f; }
+    make_frame(fr);
+    for (int k = 0; k < 9; k++) out[1896 + 9 * lane + k] = v ? fr[k] : 0.f;
     out[2184 + lane] = v ? (float)s.con_pair[lane] : -1.f;
   }
   for (int r = lane; r < MAXEFC; r += 64) {
@@ -775,6 +786,16 @@ static int build_model(const Blob& B, DModel& m, Packer& P) {
   }
   m.ntouch = (int)ts.size();
   P.add(&m.touch_site, ts); P.add(&m.touch_adr, ts); P.add(&m.touch_type, ttype); P.add(&m.touch_size, tsize);
+  {
+    // per-object "some parameter overrides this" flags (kinematics applies those overrides inline)
+    std::vector<int> bo(nbody, 0), so(std::max(nsite, 1), 0), go(std::max(m.ngeom, 1), 0);
+    for (int p = 0; p < m.nparam; p++) {
+      if (pf[p] == 0 || pf[p] == 1 || pf[p] == 3) bo[po[p]] = 1;
+      else if (pf[p] == 2) so[po[p]] = 1;
+      else if (pf[p] == 4 || pf[p] == 5) go[po[p]] = 1;
+    }
+    P.add(&m.body_ovr, bo); P.add(&m.site_ovr, so); P.add(&m.geom_ovr, go);
+  }
   P.add(&m.task_idx, tidx); P.add(&m.param_field, pf); P.add(&m.param_obj, po); P.add(&m.param_comp, pc);
   P.add(&m.act_mid, tof(B.f("task_act_mid"))); P.add(&m.act_rng, tof(B.f("task_act_rng")));
   P.add(&m.param_default, tof(B.f("task_param_default")));

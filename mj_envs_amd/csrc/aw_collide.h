@@ -35,9 +35,7 @@ AW_DEV void emit(Emit& e, float dist, const float* pos, const float* n) {
     e.s->con_pair[slot] = e.pair;
     e.s->con_dist[slot] = dist;
     copy3(e.s->con_pos[slot], pos);
-    float* f = e.s->con_frame[slot];
-    f[0] = n[0]; f[1] = n[1]; f[2] = n[2];
-    f[3] = f[4] = f[5] = 0.f;
+    copy3(e.s->con_nrm[slot], n);
   } else {
     atomicOr(&e.s->status, (unsigned)ST_CON_OVERFLOW);
   }
@@ -719,7 +717,12 @@ AW_DEV void collide_pair(const DModel& m, Env& s, int pair) {
     a.size[k] = s.gsize[g1][k]; b.size[k] = s.gsize[g2][k];
   }
   float margin = m.cp_margin[pair];   // the bounding-sphere test ran in the broadphase
-  for (int k = 0; k < 9; k++) { a.mat[k] = s.gxmat[g1][k]; b.mat[k] = s.gxmat[g2][k]; }
+  {
+    float q1[4], q2[4];
+    for (int k = 0; k < 4; k++) { q1[k] = s.gxquat[g1][k]; q2[k] = s.gxquat[g2][k]; }
+    q2m(a.mat, q1);
+    q2m(b.mat, q2);
+  }
   Emit e{&s, pair, 0};
   // every non-plane pair with a cylinder goes through MPR (mjc_Convex); one inlined call site
   if (a.type != GEOM_PLANE && (a.type == GEOM_CYLINDER || b.type == GEOM_CYLINDER)) {

@@ -23,7 +23,7 @@ constexpr int MAXT = 44;      // tendons
 constexpr int MAXU = 30;      // actuators
 constexpr int MAXCON = 32;    // contacts kept per env (oracle uses the same cap)
 constexpr int MAXEFC = 128;   // constraint rows
-constexpr int MAXDENSE = 64;  // dense (contact) constraint rows; also the noslip edge cap
+constexpr int MAXDENSE = 48;  // dense (contact) constraint rows: 12 pyramidal condim-3 contacts
 constexpr int MAXP = 8;       // per-env model parameters
 constexpr int MAXLEV = 16;    // kinematic tree depth
 constexpr int MAXTOUCH = 4;   // task touch sensors
@@ -134,70 +134,71 @@ struct DModel {
   const int* cp_class; const float* cp_rb;
   int cls_start[NCLASS + 1];  // class c owns list slots [cls_start[c], cls_start[c+1])
 
+  const int* body_ovr; const int* site_ovr; const int* geom_ovr;   // 1: some param overrides it
   const int* task_idx; const int* param_field; const int* param_obj; const int* param_comp;
   const float* act_mid; const float* act_rng; const float* param_default;
   const float* draw_lo; const float* draw_hi;
 };
 
 // ---------------------------------------------------------------------------------------
-// Per-env working set in LDS (one wave per workgroup, one env per wave).
+// Per-env working set in LDS (one wave per workgroup, one env per wave).  Sized to stay under
+// 20 KiB so EIGHT envs share a CU (two waves per SIMD: the second wave issues while the first
+// waits on LDS / L1, and VALU issue doubles from one-per-4-cycles to one-per-2).  Storage is
+// overlaid by liveness within a substep:
+//   persistent   state, body / site frames read by the task layer, per-env overrides
+//   contacts     collision -> touch sensor
+//   rows         constraint rows + dense contact Jacobian: constraints -> end of forward
+//   phase K      kinematics / com / RNE / CRB temporaries, dead once the Jacobian exists
+//   phase S      packed Cholesky factor and solver vectors (smooth solve, Newton, noslip, Euler)
+// dof vectors with only lane-local use (qacc, qacc_smooth, qfrc_smooth, qfrc_con) are VGPRs.
+constexpr int NPACK = MAXV * (MAXV + 1) / 2;   // packed lower triangle, row j at j(j+1)/2
+AW_DEV constexpr int tri(int j) { return j * (j + 1) / 2; }
+
 struct __attribute__((aligned(16))) Env {
-  // state and lane-per-dof vectors
-  float qpos[MAXV], qvel[MAXV], warm[MAXV], ctrl[MAXV];
-  float qacc[MAXV], qacc_smooth[MAXV], qfrc_smooth[MAXV], qfrc_con[MAXV], vec[MAXV], vec2[MAXV];
-  // per-env copies of the overridable model fields
-  float bpos[MAXB][3], bquat[MAXB][4], bmass[MAXB];
-  float spos[MAXS][3];
-  float gpos[MAXG][3], gsize[MAXG][3];
-  // position stage (kept through the step: obs/reward read these after the last substep)
-  float xpos[MAXB][3], xquat[MAXB][4], xmat[MAXB][9];
-  // stage arrays that are dead once the constraint rows exist; their storage is reused by
-  // the noslip pass for X = inv(M) J_edges'
   union {
-    struct {
+    struct {  // phase K
       float xipos[MAXB][3], subcom[MAXB][3];
-      float cinert[MAXB][10];
-      union {
-        struct { float crb[MAXB][10]; float buf[MAXV][6]; } p;     // M build
-        struct { float cvel[MAXB][6]; float cacc[MAXB][6]; } v;    // velocity stage (cacc -> cfrc)
-      } u1;
-      union {
-        struct { float xaxis[MAXV][3]; float xanchor[MAXV][3]; } j;
-        float cdof_dot[MAXV][6];
-      } u2;
+      float cinert[MAXB][10];   // cinert; overwritten in place by crb once RNE is done
       float cdof[MAXV][6];
-      float gxpos[MAXG][3], gxmat[MAXG][9];
+      union {
+        struct { float gxpos[MAXG][3], gxquat[MAXG][4], xaxis[MAXV][3], xanchor[MAXV][3]; };  // kin -> com
+        struct { float cvel[MAXB][6], cacc[MAXB][6]; };                                      // RNE
+        float buf[MAXV][6];                                                                   // CRB
+      };
     };
-    float X[MAXDENSE][VS];
+    struct {  // phase S
+      float4 colbuf[16];      // Cholesky column broadcast (64 floats, 16-byte aligned for b128 reads)
+      float L[NPACK];         // Cholesky factor, packed lower triangle
+      float vec[MAXV], vec2[MAXV], hdiag[MAXV];
+    };
   };
+  // persistent
+  float qpos[MAXV], qvel[MAXV], warm[MAXV], ctrl[MAXV];
+  float xpos[MAXB][3], xquat[MAXB][4];
   float sxpos[MAXS][3];
   float txmat[MAXTOUCH][9];
-  float tlen[MAXT];
-  float L[MAXV][VS];      // Cholesky rows (M, then H, then M + hD); also sparse-H staging
-  float4 colbuf[16];      // Cholesky column broadcast (64 floats, 16-byte aligned for b128 reads)
-  // contacts
+  float gsize[MAXG][3];     // per-env copy (overridable, read by every collider)
+  float bmass[MAXB];        // per-env copy (overridable, subtree sums)
+  float prm[MAXP];          // this env's model parameters
+  float touch[MAXTOUCH];
+  // contacts (normal only: the tangent frame is rebuilt where it is used)
   int ncon;
   int con_key[MAXCON], con_pair[MAXCON], con_efc[MAXCON];
-  float con_dist[MAXCON], con_pos[MAXCON][3], con_frame[MAXCON][9];
+  float con_dist[MAXCON], con_pos[MAXCON][3], con_nrm[MAXCON][3];
   // constraint rows: [0, nsparse) sparse (<= 2 nonzeros), [nsparse, nefc) dense (J rows)
-  int nefc, nsparse, ndense, npyr0;   // npyr0: first pyramidal dense row
-  unsigned char efc_type[MAXEFC];
+  int nefc, nsparse, ndense;
+  unsigned char efc_type[MAXEFC], efc_id[MAXEFC];
   signed char efc_i0[MAXEFC], efc_i1[MAXEFC];
-  short efc_id[MAXEFC];
-  float efc_v0[MAXEFC], efc_v1[MAXEFC], efc_pm[MAXEFC], efc_floss[MAXEFC], efc_D[MAXEFC];
-  float efc_aref[MAXEFC], efc_dA[MAXEFC], efc_force[MAXEFC];
+  float efc_v0[MAXEFC], efc_v1[MAXEFC], efc_floss[MAXEFC], efc_D[MAXEFC];
+  float efc_aref[MAXEFC], efc_force[MAXEFC];
   float J[MAXDENSE][VS];
   float rowbuf[MAXEFC];
-  float ns_a[MAXDENSE][3];   // noslip: per pyramid edge pair A11, A22, A12 (stored at first edge)
-  float touch[MAXTOUCH];
   unsigned status;
   int it_newton, it_noslip;   // iterations of the last solve (introspection)
 #ifdef AW_STAGE_PROF
   unsigned long long prof_acc[AW_NPROF];
   unsigned long long prof_t;
 #endif
-  int red_i;
-  float red_f[4];
 };
 
 // ---------------------------------------------------------------------------------------

@@ -10,51 +10,55 @@
 namespace aw {
 
 // ---------------------------------------------------------------------------------------
-// stage the per-env model copies (body_pos/quat/mass, site_pos, geom_pos/size) + overrides
+// this env's parameters + the per-env copies of the overridable fields read in hot loops
+// (geom_size: every collider; body_mass: subtree sums); other overrides are applied where
+// the field is read (apply_ovr)
 AW_DEV void stage_model(const DModel& m, Env& s, const float* params, int lane) {
-  for (int b = lane; b < m.nbody; b += 64) {
-    for (int k = 0; k < 3; k++) s.bpos[b][k] = m.body_pos[3 * b + k];
-    for (int k = 0; k < 4; k++) s.bquat[b][k] = m.body_quat[4 * b + k];
-    s.bmass[b] = m.body_mass[b];
-  }
-  for (int i = lane; i < m.nsite; i += 64)
-    for (int k = 0; k < 3; k++) s.spos[i][k] = m.site_pos[3 * i + k];
+  if (lane < m.nparam) s.prm[lane] = params ? params[lane] : m.param_default[lane];
+  for (int b = lane; b < m.nbody; b += 64) s.bmass[b] = m.body_mass[b];
   for (int g = lane; g < m.ngeom; g += 64)
-    for (int k = 0; k < 3; k++) { s.gpos[g][k] = m.geom_pos[3 * g + k]; s.gsize[g][k] = m.geom_size[3 * g + k]; }
+    for (int k = 0; k < 3; k++) s.gsize[g][k] = m.geom_size[3 * g + k];
   wsync();
   if (lane == 0) {
     for (int p = 0; p < m.nparam; p++) {
-      float v = params ? params[p] : m.param_default[p];
       int o = m.param_obj[p], c = m.param_comp[p];
-      switch (m.param_field[p]) {
-        case 0: s.bpos[o][c] = v; break;
-        case 1: s.bquat[o][c] = v; break;
-        case 2: s.spos[o][c] = v; break;
-        case 3: s.bmass[o] = v; break;
-        case 4: s.gpos[o][c] = v; break;
-        case 5: s.gsize[o][c] = v; break;
-      }
+      if (m.param_field[p] == 3) s.bmass[o] = s.prm[p];
+      else if (m.param_field[p] == 5) s.gsize[o][c] = s.prm[p];
     }
   }
   wsync();
 }
+// v[0..N) = model field (field code, object) with this env's overrides applied
+template <int N>
+AW_DEV void apply_ovr(const DModel& m, const Env& s, int field, int obj, float (&v)[N]) {
+  for (int p = 0; p < m.nparam; p++)
+    if (m.param_field[p] == field && m.param_obj[p] == obj) {
+      const int c = m.param_comp[p];
+      const float x = s.prm[p];
+#pragma unroll
+      for (int k = 0; k < N; k++) v[k] = k == c ? x : v[k];
+    }
+}
 
-// mj_kinematics (+ local2global for geoms, sites)
+// mj_kinematics (+ local2global for geoms, sites).  Frames are kept as quaternions only: every
+// position update rotates by the (normalised) quaternion instead of a stored rotation matrix.
 AW_DEV void stage_kinematics(const DModel& m, Env& s, int lane) {
   if (lane == 0) {
     s.xpos[0][0] = s.xpos[0][1] = s.xpos[0][2] = 0;
     s.xquat[0][0] = 1; s.xquat[0][1] = s.xquat[0][2] = s.xquat[0][3] = 0;
-    for (int k = 0; k < 9; k++) s.xmat[0][k] = (k % 4 == 0) ? 1.f : 0.f;
   }
   wsync();
   for (int lev = 1; lev < m.nlevel; lev++) {
     int beg = m.level_start[lev], end = m.level_start[lev + 1];
     for (int idx = beg + lane; idx < end; idx += 64) {
       int b = m.level_body[idx], p = m.body_parentid[b];
-      float xp[3], xq[4];
-      mulmv3(xp, s.xmat[p], s.bpos[b]);
+      float xp[3], xq[4], bp[3], bq[4], pq[4];
+      for (int k = 0; k < 3; k++) bp[k] = m.body_pos[3 * b + k];
+      for (int k = 0; k < 4; k++) { bq[k] = m.body_quat[4 * b + k]; pq[k] = s.xquat[p][k]; }
+      if (m.body_ovr[b]) { apply_ovr<3>(m, s, 0, b, bp); apply_ovr<4>(m, s, 1, b, bq); }
+      rotvq(xp, bp, pq);
       add3(xp, xp, s.xpos[p]);
-      mulq(xq, s.xquat[p], s.bquat[b]);
+      mulq(xq, pq, bq);
       int da = m.body_dofadr[b];
       for (int k = 0; k < m.body_dofnum[b]; k++) {
         int j = da + k;
@@ -75,30 +79,34 @@ AW_DEV void stage_kinematics(const DModel& m, Env& s, int lane) {
           rotvq(v, jp, xq);
           sub3(xp, xanchor, v);
         }
-        copy3(s.u2.j.xaxis[j], xaxis);
-        copy3(s.u2.j.xanchor[j], xanchor);
+        copy3(s.xaxis[j], xaxis);
+        copy3(s.xanchor[j], xanchor);
       }
       normq(xq);
       copy3(s.xpos[b], xp);
       for (int c = 0; c < 4; c++) s.xquat[b][c] = xq[c];
-      q2m(s.xmat[b], xq);
     }
     wsync();
   }
   // geoms (compact collidable list), sites, inertial frames
   for (int g = lane; g < m.ngeom; g += 64) {
     int b = m.geom_bodyid[g];
-    float v[3], q[4], gq[4];
-    mulmv3(v, s.xmat[b], s.gpos[g]);
+    float v[3], q[4], gq[4], gp[3], bq[4];
+    for (int c = 0; c < 3; c++) gp[c] = m.geom_pos[3 * g + c];
+    if (m.geom_ovr[g]) apply_ovr<3>(m, s, 4, g, gp);
+    for (int c = 0; c < 4; c++) { gq[c] = m.geom_quat[4 * g + c]; bq[c] = s.xquat[b][c]; }
+    rotvq(v, gp, bq);
     add3(s.gxpos[g], v, s.xpos[b]);
-    for (int c = 0; c < 4; c++) gq[c] = m.geom_quat[4 * g + c];
-    mulq(q, s.xquat[b], gq);
-    q2m(s.gxmat[g], q);
+    mulq(q, bq, gq);
+    for (int c = 0; c < 4; c++) s.gxquat[g][c] = q[c];
   }
   for (int i = lane; i < m.nsite; i += 64) {
     int b = m.site_bodyid[i];
-    float v[3];
-    mulmv3(v, s.xmat[b], s.spos[i]);
+    float v[3], sp[3], bq[4];
+    for (int c = 0; c < 3; c++) sp[c] = m.site_pos[3 * i + c];
+    if (m.site_ovr[i]) apply_ovr<3>(m, s, 2, i, sp);
+    for (int c = 0; c < 4; c++) bq[c] = s.xquat[b][c];
+    rotvq(v, sp, bq);
     add3(s.sxpos[i], v, s.xpos[b]);
   }
   if (lane < m.ntouch) {
@@ -109,9 +117,10 @@ AW_DEV void stage_kinematics(const DModel& m, Env& s, int lane) {
     q2m(s.txmat[lane], q);
   }
   for (int b = lane; b < m.nbody; b += 64) {
-    float v[3], ip[3];
+    float v[3], ip[3], bq[4];
     for (int c = 0; c < 3; c++) ip[c] = m.body_ipos[3 * b + c];
-    mulmv3(v, s.xmat[b], ip);
+    for (int c = 0; c < 4; c++) bq[c] = s.xquat[b][c];
+    rotvq(v, ip, bq);
     add3(s.xipos[b], v, s.xpos[b]);
   }
   wsync();
@@ -156,49 +165,47 @@ AW_DEV void stage_com(const DModel& m, Env& s, int lane) {
   if (lane < m.nv) {
     int j = lane, b = m.dof_bodyid[j];
     float* cd = s.cdof[j];
-    const float* axis = s.u2.j.xaxis[j];
+    const float* axis = s.xaxis[j];
     if (m.jnt_type[j] == JNT_SLIDE) {
       cd[0] = cd[1] = cd[2] = 0;
       copy3(cd + 3, axis);
     } else {
       float off[3];
-      sub3(off, s.subcom[m.body_rootid[b]], s.u2.j.xanchor[j]);
+      sub3(off, s.subcom[m.body_rootid[b]], s.xanchor[j]);
       copy3(cd, axis);
       cross3(cd + 3, axis, off);
     }
   }
-  for (int t = lane; t < m.ntendon; t += 64) {
-    int d1 = m.ten_d1[t];
-    s.tlen[t] = m.ten_c0[t] * s.qpos[m.ten_d0[t]] + (d1 >= 0 ? m.ten_c1[t] * s.qpos[d1] : 0.f);
-  }
   wsync();
 }
 
-// mj_crb -> M row per lane (registers).  M[i][k] = cdof_k . (crb_{body i} cdof_i) for k an
-// ancestor of i, symmetric for descendants, + armature on the diagonal.
+// mj_crb -> M row per lane (registers).  Runs after RNE: the composite inertias overwrite
+// cinert in place.  M[i][k] = cdof_k . (crb_{body i} cdof_i) for k an ancestor of i, symmetric
+// for descendants, + armature on the diagonal.
 template <int NV>
 AW_DEV void stage_crb(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
-  for (int b = lane; b < m.nbody; b += 64) {
-    float acc[10];
-    for (int k = 0; k < 10; k++) acc[k] = 0;
-    if (b > 0)
-      for (int d = b; d < m.body_subtree_end[b]; d++)
-        for (int k = 0; k < 10; k++) acc[k] += s.cinert[d][k];
-    for (int k = 0; k < 10; k++) s.u1.p.crb[b][k] = acc[k];
-  }
+  float acc[10];
+  for (int k = 0; k < 10; k++) acc[k] = 0;
+  const int bb = lane < m.nbody ? lane : 0;
+  if (lane < m.nbody && lane > 0)
+    for (int d = bb; d < m.body_subtree_end[bb]; d++)
+      for (int k = 0; k < 10; k++) acc[k] += s.cinert[d][k];
+  wsync();
+  if (lane < m.nbody)
+    for (int k = 0; k < 10; k++) s.cinert[bb][k] = acc[k];
   wsync();
   const int li = lane < NV ? lane : NV - 1;
   float ci[6], bi[6];
   for (int k = 0; k < 6; k++) ci[k] = s.cdof[li][k];
-  mul_inert_vec(bi, s.u1.p.crb[m.dof_bodyid[li]], ci);
-  for (int k = 0; k < 6; k++) s.u1.p.buf[li][k] = bi[k];
+  mul_inert_vec(bi, s.cinert[m.dof_bodyid[li]], ci);
+  for (int k = 0; k < 6; k++) s.buf[li][k] = bi[k];
   wsync();
   const unsigned long long anc = m.dof_ancmask[li];
   const float arm = m.dof_armature[li];
 #pragma unroll
   for (int k = 0; k < NV; k++) {
     float ck[6], bk[6];
-    for (int c = 0; c < 6; c++) { ck[c] = s.cdof[k][c]; bk[c] = s.u1.p.buf[k][c]; }
+    for (int c = 0; c < 6; c++) { ck[c] = s.cdof[k][c]; bk[c] = s.buf[k][c]; }
     const unsigned long long anck = m.dof_ancmask[k];
     float v;
     if (k == li) v = dot6(ci, bi) + arm;
@@ -210,10 +217,10 @@ AW_DEV void stage_crb(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
   wsync();
 }
 
-// mj_comVel + mj_rne(flg_acc=0) + mj_passive + mj_fwdActuation -> qfrc_smooth
-AW_DEV void stage_velocity(const DModel& m, Env& s, int lane) {
-  float (*cvel)[6] = s.u1.v.cvel;
-  float (*cacc)[6] = s.u1.v.cacc;
+// mj_comVel + mj_rne(flg_acc=0) + mj_passive + mj_fwdActuation -> qfrc_smooth (lane = dof)
+AW_DEV float stage_velocity(const DModel& m, Env& s, int lane) {
+  float (*cvel)[6] = s.cvel;
+  float (*cacc)[6] = s.cacc;
   if (lane == 0) {
     for (int k = 0; k < 6; k++) { cvel[0][k] = 0; cacc[0][k] = 0; }
     if (!(m.disableflags & DSBL_GRAVITY)) { cacc[0][3] = -m.gravity[0]; cacc[0][4] = -m.gravity[1]; cacc[0][5] = -m.gravity[2]; }
@@ -231,7 +238,7 @@ AW_DEV void stage_velocity(const DModel& m, Env& s, int lane) {
         float cd[6], cdd[6], qv = s.qvel[j];
         for (int k = 0; k < 6; k++) cd[k] = s.cdof[j][k];
         cross_motion(cdd, cv, cd);
-        for (int k = 0; k < 6; k++) { s.u2.cdof_dot[j][k] = cdd[k]; cv[k] += cd[k] * qv; ca[k] += cdd[k] * qv; }
+        for (int k = 0; k < 6; k++) { cv[k] += cd[k] * qv; ca[k] += cdd[k] * qv; }
       }
       for (int k = 0; k < 6; k++) { cvel[b][k] = cv[k]; cacc[b][k] = ca[k]; }
     }
@@ -259,6 +266,7 @@ AW_DEV void stage_velocity(const DModel& m, Env& s, int lane) {
   if (lane < m.nbody)
     for (int k = 0; k < 6; k++) cvel[bb][k] = sub[k];
   wsync();
+  float qfrc = 0.f;
   if (lane < m.nv) {
     int j = lane;
     float bias = dot6(s.cdof[j], cvel[m.dof_bodyid[j]]);
@@ -276,9 +284,10 @@ AW_DEV void stage_velocity(const DModel& m, Env& s, int lane) {
       if (m.act_forcelimited[u]) f = clampf(f, m.act_forcerange[2 * u], m.act_forcerange[2 * u + 1]);
       act = gear * f;
     }
-    s.qfrc_smooth[j] = pas - bias + act;
+    qfrc = pas - bias + act;
   }
   wsync();
+  return qfrc;
 }
 
 }  // namespace aw

@@ -55,10 +55,10 @@ AW_DEV void chol_store(const float (&row)[NV], int lane, Env& s) {
   if (lane < NV) {
 #pragma unroll
     for (int k = 0; k < NV; k++)
-      if (k <= lane) s.L[lane][k] = row[k];
+      if (k <= lane) s.L[tri(lane) + k] = row[k];
   }
 }
-// x = inv(L L') b, b lane-distributed; L rows in registers (forward) and in LDS (backward)
+// x = inv(L L') b, b lane-distributed; L rows in registers (forward) and packed in LDS (backward)
 template <int NV>
 AW_DEV float chol_solve(const float (&row)[NV], float invd, float b, int lane, const Env& s) {
 #pragma unroll
@@ -71,7 +71,7 @@ AW_DEV float chol_solve(const float (&row)[NV], float invd, float b, int lane, c
   for (int j = NV - 1; j >= 0; j--) {
     float xj = rlane(b, j) * rlane(invd, j);
     if (lane == j) b = xj;
-    else if (lane < j) b = fmaf(-s.L[j][lane], xj, b);
+    else if (lane < j) b = fmaf(-s.L[tri(j) + lane], xj, b);
   }
   return lane < NV ? b : 0.f;
 }
@@ -146,7 +146,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
     int d = m.fl_dof[lane];
     s.efc_type[lane] = C_FRIC_DOF; s.efc_id[lane] = d;
     s.efc_i0[lane] = d; s.efc_i1[lane] = -1; s.efc_v0[lane] = 1.f; s.efc_v1[lane] = 0.f;
-    s.efc_pm[lane] = 0.f; s.efc_floss[lane] = m.dof_frictionloss[d]; s.efc_dA[lane] = m.dof_invweight0[d];
+    s.rowbuf[lane] = 0.f; s.efc_floss[lane] = m.dof_frictionloss[d]; s.efc_force[lane] = m.dof_invweight0[d];
   }
   // joint limits: lower then upper per joint, joints in order
   const bool lim = !(m.disableflags & DSBL_LIMIT);
@@ -168,13 +168,14 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
       if (r >= MAXEFC) { atomicOr(&s.status, (unsigned)ST_EFC_OVERFLOW); continue; }
       s.efc_type[r] = C_LIM_JNT; s.efc_id[r] = lane;
       s.efc_i0[r] = lane; s.efc_i1[r] = -1; s.efc_v0[r] = side ? -1.f : 1.f; s.efc_v1[r] = 0.f;
-      s.efc_pm[r] = (side ? dhi : dlo) - mg; s.efc_floss[r] = 0.f; s.efc_dA[r] = m.dof_invweight0[lane];
+      s.rowbuf[r] = (side ? dhi : dlo) - mg; s.efc_floss[r] = 0.f; s.efc_force[r] = m.dof_invweight0[lane];
     }
   }
   // tendon limits
   lo = hi = 0;
   if (lim && lane < m.ntendon && m.ten_limited[lane]) {
-    float len = s.tlen[lane];
+    const int d1 = m.ten_d1[lane];
+    float len = m.ten_c0[lane] * s.qpos[m.ten_d0[lane]] + (d1 >= 0 ? m.ten_c1[lane] * s.qpos[d1] : 0.f);
     mg = m.ten_margin[lane];
     dlo = len - m.ten_range[2 * lane];
     dhi = m.ten_range[2 * lane + 1] - len;
@@ -191,7 +192,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
       s.efc_type[r] = C_LIM_TEN; s.efc_id[r] = lane;
       s.efc_i0[r] = m.ten_d0[lane]; s.efc_i1[r] = m.ten_d1[lane];
       s.efc_v0[r] = sg * m.ten_c0[lane]; s.efc_v1[r] = sg * m.ten_c1[lane];
-      s.efc_pm[r] = (side ? dhi : dlo) - mg; s.efc_floss[r] = 0.f; s.efc_dA[r] = m.ten_invweight0[lane];
+      s.rowbuf[r] = (side ? dhi : dlo) - mg; s.efc_floss[r] = 0.f; s.efc_force[r] = m.ten_invweight0[lane];
     }
   }
   int nsparse = nfl + njl + ntl;
@@ -222,15 +223,15 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
     float pm = s.con_dist[lane] - (m.cp_margin[pair] - m.cp_gap[pair]);
     int r = nsparse + doff;
     if (dim == 1) {
-      s.efc_type[r] = C_CON_FRICTIONLESS; s.efc_id[r] = lane; s.efc_pm[r] = pm; s.efc_floss[r] = 0.f;
-      s.efc_dA[r] = tran; s.efc_i0[r] = 0; s.efc_i1[r] = 0;
+      s.efc_type[r] = C_CON_FRICTIONLESS; s.efc_id[r] = lane; s.rowbuf[r] = pm; s.efc_floss[r] = 0.f;
+      s.efc_force[r] = tran; s.efc_i0[r] = 0; s.efc_i1[r] = 0;
     } else {
       for (int k = 1; k < dim; k++) {
         float fri = m.cp_friction[5 * pair + k - 1];
         float dA = tran + fri * fri * (k < 3 ? tran : rot);
         for (int sd = 0; sd < 2; sd++) {
-          s.efc_type[r] = C_CON_PYRAMIDAL; s.efc_id[r] = lane; s.efc_pm[r] = pm; s.efc_floss[r] = 0.f;
-          s.efc_dA[r] = dA; s.efc_i0[r] = k; s.efc_i1[r] = sd ? -1 : 1;
+          s.efc_type[r] = C_CON_PYRAMIDAL; s.efc_id[r] = lane; s.rowbuf[r] = pm; s.efc_floss[r] = 0.f;
+          s.efc_force[r] = dA; s.efc_i0[r] = k; s.efc_i1[r] = sd ? -1 : 1;
           r++;
         }
       }
@@ -248,7 +249,9 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
       int k = lane;
       int b1 = m.geom_bodyid[m.cp_g1[pr]], b2 = m.geom_bodyid[m.cp_g2[pr]];
       const float* pos = s.con_pos[c];
-      const float* fr = s.con_frame[c];
+      float fr[9];
+      for (int q = 0; q < 3; q++) { fr[q] = s.con_nrm[c][q]; fr[3 + q] = 0.f; }
+      make_frame(fr);
       const float* cd = s.cdof[k];
       float jp[3] = {0, 0, 0}, jr[3] = {0, 0, 0};
       if ((m.body_dofmask[b2] >> k) & 1ull) {
@@ -287,7 +290,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
     else if (t == C_LIM_JNT) { solref = &m.jnt_solref[2 * id]; solimp = &m.jnt_solimp[5 * id]; }
     else if (t == C_LIM_TEN) { solref = &m.ten_solref[2 * id]; solimp = &m.ten_solimp[5 * id]; }
     else { int pr = s.con_pair[id]; solref = &m.cp_solref[2 * pr]; solimp = &m.cp_solimp[5 * pr]; }
-    float pm = s.efc_pm[r];
+    float pm = s.rowbuf[r];          // stashed by the row assembly above
     float imp = getimpedance(solimp, pm);
     float dmax = clampf(solimp[1], 0.0001f, 0.9999f);
     float K, B;
@@ -300,7 +303,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
       K = -solref[0] / (dmax * dmax);
       B = -solref[1] / dmax;
     }
-    float R = fmaxf((1.f - imp) * s.efc_dA[r] / imp, MINVAL);
+    float R = fmaxf((1.f - imp) * s.efc_force[r] / imp, MINVAL);
     s.efc_D[r] = 1.f / R;
     float vel = row_dot<NV>(s, r, s.qvel);
     s.efc_aref[r] = -B * vel - K * imp * pm;
@@ -330,10 +333,11 @@ AW_DEV float row_eval(const RowR& r, float jar, float* force, int* st) {
 }
 
 template <int NV>
-AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[NV], float& a) {
+AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[NV], float& a, float qfrc_smooth,
+                         float qacc_smooth) {
   const int nefc = s.nefc;
-  const float fs = lane < NV ? s.qfrc_smooth[lane] : 0.f;
-  const float a0 = lane < NV ? s.qacc_smooth[lane] : 0.f;
+  const float fs = lane < NV ? qfrc_smooth : 0.f;
+  const float a0 = lane < NV ? qacc_smooth : 0.f;
   RowR rr[2];
   for (int h = 0; h < 2; h++) {
     int r = lane + 64 * h;
@@ -386,30 +390,47 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
   AW_PROF(s, PR_NT_INIT);
   int iter = 0;
   for (; iter < m.iterations; iter++) {
-    // Hessian H = M + J' D_quad J
-    for (int idx = lane; idx < NV * VS; idx += 64) (&s.L[0][0])[idx] = 0.f;
+    // Hessian H = M + J' D_quad J.  Sparse rows: diagonal terms gathered through an LDS vector,
+    // the off-diagonal term of a two-dof (tendon) row added in registers by the two lanes it
+    // couples; dense rows: rank-1 updates with the row broadcast from LDS.
+    if (lane < NV) s.hdiag[lane] = 0.f;
     wsync();
+    unsigned long long offd[2];
     for (int h = 0; h < 2; h++) {
       int r = lane + 64 * h;
-      if (r >= nefc) continue;
-      float w = rr[h].st == S_QUAD ? rr[h].D : 0.f;
-      s.rowbuf[r] = w;
-      if (r < s.nsparse && w != 0.f) {
-        int i0 = s.efc_i0[r], i1 = s.efc_i1[r];
-        float v0 = s.efc_v0[r], v1 = s.efc_v1[r];
-        atomicAdd(&s.L[i0][i0], w * v0 * v0);
-        if (i1 >= 0) {
-          atomicAdd(&s.L[i0][i1], w * v0 * v1);
-          atomicAdd(&s.L[i1][i0], w * v0 * v1);
-          atomicAdd(&s.L[i1][i1], w * v1 * v1);
+      bool od = false;
+      if (r < nefc) {
+        float w = rr[h].st == S_QUAD ? rr[h].D : 0.f;
+        s.rowbuf[r] = w;
+        if (r < s.nsparse && w != 0.f) {
+          int i0 = s.efc_i0[r], i1 = s.efc_i1[r];
+          float v0 = s.efc_v0[r], v1 = s.efc_v1[r];
+          atomicAdd(&s.hdiag[i0], w * v0 * v0);
+          if (i1 >= 0) { atomicAdd(&s.hdiag[i1], w * v1 * v1); od = true; }
         }
       }
+      offd[h] = __ballot(od);
     }
     wsync();
     float H[NV];
     const int li = lane < NV ? lane : NV - 1;
+    {
+      const float dg = s.hdiag[li];
 #pragma unroll
-    for (int k = 0; k < NV; k++) H[k] = Mrow[k] + s.L[li][k];
+      for (int k = 0; k < NV; k++) H[k] = Mrow[k] + (k == lane ? dg : 0.f);
+    }
+    for (int h = 0; h < 2; h++) {
+      while (offd[h]) {
+        const int r = 64 * h + __builtin_ctzll(offd[h]);
+        offd[h] &= offd[h] - 1ull;
+        const int i0 = __builtin_amdgcn_readfirstlane(s.efc_i0[r]);
+        const int i1 = __builtin_amdgcn_readfirstlane(s.efc_i1[r]);
+        const float val = s.rowbuf[r] * s.efc_v0[r] * s.efc_v1[r];
+        const int other = lane == i0 ? i1 : (lane == i1 ? i0 : -1);
+#pragma unroll
+        for (int k = 0; k < NV; k++) H[k] += k == other ? val : 0.f;
+      }
+    }
     for (int d = 0; d < s.ndense; d++) {
       float w = s.rowbuf[s.nsparse + d];
       if (w == 0.f) continue;
@@ -516,7 +537,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
   for (int j = 0; j < NV; j++) {
     float acc = (j == lane) ? 1.f : 0.f;
 #pragma unroll
-    for (int k = 0; k < j; k++) acc = fmaf(-s.L[j][k], Mi[k], acc);
+    for (int k = 0; k < j; k++) acc = fmaf(-s.L[tri(j) + k], Mi[k], acc);
     Mi[j] = acc * s.vec2[j];
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -524,7 +545,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
   for (int j = NV - 1; j >= 0; j--) {
     float acc = Mi[j];
 #pragma unroll
-    for (int k = j + 1; k < NV; k++) acc = fmaf(-s.L[k][j], Mi[k], acc);
+    for (int k = j + 1; k < NV; k++) acc = fmaf(-s.L[tri(k) + j], Mi[k], acc);
     Mi[j] = acc * s.vec2[j];
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -536,23 +557,6 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
   const float lm = lane < NV ? 1.f : 0.f;
   wsync();
   AW_PROF(s, PR_NS_MINV);
-  // X[e][k] = (inv(M) J_e')_k for pyramidal dense rows (LDS, overlays dead stage arrays)
-  for (int e = 0; e < ndense; e++) {
-    if (s.efc_type[nsparse + e] != C_CON_PYRAMIDAL) continue;
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < NV; j++) acc = fmaf(Mi[j], s.J[e][j], acc);
-    if (lane < NV) s.X[e][lane] = acc;
-  }
-  wsync();
-  // pair constants A11, A22, A12 of each opposing edge pair
-  for (int e = 0; e + 1 < ndense; e++) {
-    if (!(s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1)) continue;
-    float j1 = lm * s.J[e][li], j2 = lm * s.J[e + 1][li];
-    float x1 = lm * s.X[e][li], x2 = lm * s.X[e + 1][li];
-    float a11 = wave_sum(j1 * x1), a22 = wave_sum(j2 * x2), a12 = wave_sum(j1 * x2);
-    if (lane == 0) { s.ns_a[e][0] = a11; s.ns_a[e][1] = a22; s.ns_a[e][2] = a12; }
-  }
   // forces: frictionloss rows per dof lane, dense rows per lane
   const bool use_fl = !(m.disableflags & DSBL_FRICTIONLOSS);
   float ffl = 0.f, fd = 0.f;
@@ -575,44 +579,41 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
     }
   }
   if (lane < ndense) fd = s.efc_force[nsparse + lane];
-  wsync();
   qacc = lane < NV ? qacc : 0.f;
   const float scale = 1.f / (m.meaninertia * (float)(NV > 1 ? NV : 1));
-  // compact list of active edge pairs (K >= MINVAL), pair p's constants in lane p; the J / X
-  // rows of the first NSP_CACHE pairs are cached in VGPRs for the sweeps
-  int npr, pr_e = 0;
+  // opposing pyramid-edge pairs (e, e+1) in row order: x = inv(M) J_e' in registers, pair
+  // constants A11, A22, A12 by wave sums; pairs with K >= MINVAL are compacted, pair p's
+  // constants in lane p, the J / x rows of the first NSP_CACHE pairs kept in VGPRs
+  int npr = 0, pr_e = 0;
   float pr_a11 = 0.f, pr_a22 = 0.f, pr_a12 = 0.f, pr_ik = 0.f, pr_ar1 = 0.f, pr_ar2 = 0.f;
-  {
-    int* lst = reinterpret_cast<int*>(s.rowbuf);   // rowbuf is dead between Newton and jt_mul
-    const int e = lane;
-    bool act = false;
-    if (e + 1 < ndense && s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1) {
-      const float K = s.ns_a[e][0] + s.ns_a[e][1] - 2.f * s.ns_a[e][2];
-      act = K >= MINVAL;
-    }
-    const unsigned long long msk = __ballot(act);
-    if (act) lst[__popcll(msk & ((1ull << lane) - 1ull))] = e;
-    npr = __popcll(msk);
-    wsync();
-    if (lane < npr) {
-      pr_e = lst[lane];
-      pr_a11 = s.ns_a[pr_e][0]; pr_a22 = s.ns_a[pr_e][1]; pr_a12 = s.ns_a[pr_e][2];
-      pr_ik = 1.0f / (pr_a11 + pr_a22 - 2.f * pr_a12);
-      pr_ar1 = s.efc_aref[nsparse + pr_e];
-      pr_ar2 = s.efc_aref[nsparse + pr_e + 1];
-    }
-    wsync();
-  }
   float c_j1[NSP_CACHE], c_j2[NSP_CACHE], c_x1[NSP_CACHE], c_x2[NSP_CACHE];
 #pragma unroll
-  for (int p = 0; p < NSP_CACHE; p++) {
-    c_j1[p] = c_j2[p] = c_x1[p] = c_x2[p] = 0.f;
-    if (p < npr) {
-      const int e = rlane_i(pr_e, p);
-      c_j1[p] = lm * s.J[e][li]; c_j2[p] = lm * s.J[e + 1][li];
-      c_x1[p] = lm * s.X[e][li]; c_x2[p] = lm * s.X[e + 1][li];
+  for (int p = 0; p < NSP_CACHE; p++) c_j1[p] = c_j2[p] = c_x1[p] = c_x2[p] = 0.f;
+  auto edge_rows = [&](int e, float& j1, float& j2, float& x1, float& x2) {
+    j1 = lm * s.J[e][li];
+    j2 = lm * s.J[e + 1][li];
+    float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; j++) { a1 = fmaf(Mi[j], s.J[e][j], a1); a2 = fmaf(Mi[j], s.J[e + 1][j], a2); }
+    x1 = a1; x2 = a2;
+  };
+  for (int e = 0; e + 1 < ndense; e++) {
+    if (!(s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1)) continue;
+    float j1, j2, x1, x2;
+    edge_rows(e, j1, j2, x1, x2);
+    const float a11 = wave_sum(j1 * x1), a22 = wave_sum(j2 * x2), a12 = wave_sum(j1 * x2);
+    const float K = a11 + a22 - 2.f * a12;
+    if (!(K >= MINVAL)) continue;
+    const int p = npr++;
+    if (lane == p) {
+      pr_e = e; pr_a11 = a11; pr_a22 = a22; pr_a12 = a12; pr_ik = 1.0f / K;
+      pr_ar1 = s.efc_aref[nsparse + e]; pr_ar2 = s.efc_aref[nsparse + e + 1];
     }
+#pragma unroll
+    for (int q = 0; q < NSP_CACHE; q++)
+      if (q == p) { c_j1[q] = j1; c_j2[q] = j2; c_x1[q] = x1; c_x2[q] = x2; }
   }
+  wsync();
   AW_PROF(s, PR_NS_SETUP);
   if (lane == 0) s.it_noslip = 0;
   for (int it = 0; it < m.noslip_iterations; it++) {
@@ -655,8 +656,9 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
     for (int p = 0; p < NSP_CACHE; p++)
       if (p < npr) pair_step(p, c_j1[p], c_j2[p], c_x1[p], c_x2[p]);
     for (int p = NSP_CACHE; p < npr; p++) {
-      const int e = rlane_i(pr_e, p);
-      pair_step(p, lm * s.J[e][li], lm * s.J[e + 1][li], lm * s.X[e][li], lm * s.X[e + 1][li]);
+      float j1, j2, x1, x2;
+      edge_rows(rlane_i(pr_e, p), j1, j2, x1, x2);
+      pair_step(p, j1, j2, x1, x2);
     }
     if (impr * scale < m.noslip_tolerance) break;
   }
@@ -738,7 +740,7 @@ AW_DEV void stage_touch(const DModel& m, Env& s, int lane) {
         else for (int j = 0; j < 2 * (dim - 1); j++) fn += s.efc_force[adr + j];
         if (fn > 0.f) {
           float ray[3];
-          copy3(ray, s.con_frame[lane]);
+          copy3(ray, s.con_nrm[lane]);
           normalize3(ray);
           if (bid == b2) scl3(ray, ray, -1.f);
           if (ray_geom(s.sxpos[site], s.txmat[t], &m.touch_size[3 * t], s.con_pos[lane], ray, m.touch_type[t]) >= 0.f)
