@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -86,12 +87,12 @@ AW_DEV void stage_collision(const DModel& m, Env& s, int lane) {
       bool pass = false;
       int cls = -1;
       if (p < m.npairall) {
-        cls = m.cp_class[p];
-        const float rb = m.cp_rb[p];
+        cls = MD(cp_class, p);
+        const float rb = MD(cp_rb, p);
         if (rb < 0.f) {
           pass = true;
         } else {
-          const int g1 = m.cp_g1[p], g2 = m.cp_g2[p];
+          const int g1 = MD(cp_g1, p), g2 = MD(cp_g2, p);
           float dif[3];
           sub3(dif, s.gxpos[g1], s.gxpos[g2]);
           pass = !(norm3(dif) > rb);
@@ -186,7 +187,7 @@ AW_DEV void euler(const DModel& m, Env& s, int lane, const float (&Mrow)[NV], co
   float acc;
   if (dmp) {
     float row[NV];
-    const float dd = lane < NV ? h * m.dof_damping[lane] : 0.f;
+    const float dd = lane < NV ? h * MD(dof_damping, lane) : 0.f;
 #pragma unroll
     for (int k = 0; k < NV; k++) row[k] = Mrow[k] + (k == lane ? dd : 0.f);
     float invd = 1.f;
@@ -314,7 +315,7 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel m, DState st, 
   load_env<NV>(m, s, st, env, lane);
   if (lane < m.nu) {
     float a = clampf(actions[(size_t)env * m.nu + lane], -1.f, 1.f);
-    s.ctrl[lane] = m.act_mid[lane] + a * m.act_rng[lane];
+    s.ctrl[lane] = MD(act_mid, lane) + a * MD(act_rng, lane);
   }
   stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
   float Mrow[NV];
@@ -536,17 +537,16 @@ struct Blob {
   double opt(const char* name, double dflt) const { return aw_blob_opt(p, n, name, dflt); }
 };
 
-struct Packer {
-  std::vector<char> buf;
-  std::vector<std::pair<size_t, const void**>> fix;
-  template <class T>
-  void add(const T** slot, const std::vector<T>& v) {
-    size_t off = (buf.size() + 15) & ~size_t(15);
-    buf.resize(off + std::max<size_t>(v.size(), 1) * sizeof(T), 0);
-    if (!v.empty()) memcpy(buf.data() + off, v.data(), v.size() * sizeof(T));
-    fix.push_back({off, (const void**)slot});
-  }
-};
+template <class T, size_t N, class U>
+bool put_arr(T (&dst)[N], const std::vector<U>& v) {
+  if (v.size() > N) return false;
+  for (size_t i = 0; i < v.size(); i++) dst[i] = (T)v[i];
+  return true;
+}
+#define PUT(name, ...)                                                                        \
+  do {                                                                                        \
+    if (!put_arr(md.name, __VA_ARGS__)) return fail(AW_EUNSUPPORTED, "model field " #name " exceeds kernel capacity"); \
+  } while (0)
 
 std::vector<float> tof(const std::vector<double>& v) { return std::vector<float>(v.begin(), v.end()); }
 }  // namespace
@@ -559,7 +559,7 @@ struct aw_handle {
   void* dstate = nullptr;
 };
 
-static int build_model(const Blob& B, DModel& m, Packer& P) {
+static int build_model(const Blob& B, DModel& m, MData& md) {
   memset(&m, 0, sizeof(m));
   int nq = B.dim("nq"), nv = B.dim("nv"), nu = B.dim("nu"), nbody = B.dim("nbody"), njnt = B.dim("njnt");
   int ngeom_all = B.dim("ngeom"), nsite = B.dim("nsite"), ntendon = B.dim("ntendon");
@@ -617,22 +617,22 @@ static int build_model(const Blob& B, DModel& m, Packer& P) {
   for (int j = 0; j < nv; j++)
     for (int a = dparent[j]; a >= 0; a = dparent[a]) amask[j] |= 1ull << a;
 
-  P.add(&m.body_parentid, parent); P.add(&m.body_rootid, rootid); P.add(&m.body_dofnum, dofnum);
-  P.add(&m.body_dofadr, dofadr); P.add(&m.body_subtree_end, send); P.add(&m.level_start, lstart);
-  P.add(&m.level_body, lbody);
-  P.add(&m.body_pos, tof(B.f("body_pos"))); P.add(&m.body_quat, tof(B.f("body_quat")));
-  P.add(&m.body_ipos, tof(B.f("body_ipos"))); P.add(&m.body_iquat, tof(B.f("body_iquat")));
-  P.add(&m.body_mass, tof(B.f("body_mass"))); P.add(&m.body_inertia, tof(B.f("body_inertia")));
-  P.add(&m.body_invweight0, tof(B.f("body_invweight0")));
-  P.add(&m.body_subtreemass, tof(B.f("body_subtreemass")));
-  P.add(&m.body_dofmask, bmask);
+  PUT(body_parentid, parent); PUT(body_rootid, rootid); PUT(body_dofnum, dofnum);
+  PUT(body_dofadr, dofadr); PUT(body_subtree_end, send); PUT(level_start, lstart);
+  PUT(level_body, lbody);
+  PUT(body_pos, tof(B.f("body_pos"))); PUT(body_quat, tof(B.f("body_quat")));
+  PUT(body_ipos, tof(B.f("body_ipos"))); PUT(body_iquat, tof(B.f("body_iquat")));
+  PUT(body_mass, tof(B.f("body_mass"))); PUT(body_inertia, tof(B.f("body_inertia")));
+  PUT(body_invweight0, tof(B.f("body_invweight0")));
+  PUT(body_subtreemass, tof(B.f("body_subtreemass")));
+  PUT(body_dofmask, bmask);
 
   std::vector<int> jtype = B.i("jnt_type");
   for (int t : jtype) if (t != JNT_HINGE && t != JNT_SLIDE) return fail(AW_EUNSUPPORTED, "joint type");
-  P.add(&m.jnt_type, jtype); P.add(&m.jnt_bodyid, B.i("jnt_bodyid")); P.add(&m.jnt_limited, B.i("jnt_limited"));
-  P.add(&m.jnt_pos, tof(B.f("jnt_pos"))); P.add(&m.jnt_axis, tof(B.f("jnt_axis")));
-  P.add(&m.jnt_range, tof(B.f("jnt_range"))); P.add(&m.jnt_margin, tof(B.f("jnt_margin")));
-  P.add(&m.jnt_solref, tof(B.f("jnt_solref"))); P.add(&m.jnt_solimp, tof(B.f("jnt_solimp")));
+  PUT(jnt_type, jtype); PUT(jnt_bodyid, B.i("jnt_bodyid")); PUT(jnt_limited, B.i("jnt_limited"));
+  PUT(jnt_pos, tof(B.f("jnt_pos"))); PUT(jnt_axis, tof(B.f("jnt_axis")));
+  PUT(jnt_range, tof(B.f("jnt_range"))); PUT(jnt_margin, tof(B.f("jnt_margin")));
+  PUT(jnt_solref, tof(B.f("jnt_solref"))); PUT(jnt_solimp, tof(B.f("jnt_solimp")));
 
   // actuators (joint transmission, one per dof)
   std::vector<int> trn = B.i("actuator_trnid");
@@ -646,11 +646,11 @@ static int build_model(const Blob& B, DModel& m, Packer& P) {
   for (int j = 0; j < nv; j++)
     if (floss[j] > 0) { fl_row[j] = (int)fl_dof.size(); fl_dof.push_back(j); }
   m.nfl = (int)fl_dof.size();
-  P.add(&m.dof_bodyid, B.i("dof_bodyid")); P.add(&m.dof_act, dact); P.add(&m.fl_dof, fl_dof);
-  P.add(&m.fl_row, fl_row); P.add(&m.dof_ancmask, amask);
-  P.add(&m.dof_armature, tof(B.f("dof_armature"))); P.add(&m.dof_damping, tof(B.f("dof_damping")));
-  P.add(&m.dof_frictionloss, tof(floss)); P.add(&m.dof_invweight0, tof(B.f("dof_invweight0")));
-  P.add(&m.dof_solref, tof(B.f("dof_solref"))); P.add(&m.dof_solimp, tof(B.f("dof_solimp")));
+  PUT(dof_bodyid, B.i("dof_bodyid")); PUT(dof_act, dact); PUT(fl_dof, fl_dof);
+  PUT(fl_row, fl_row); PUT(dof_ancmask, amask);
+  PUT(dof_armature, tof(B.f("dof_armature"))); PUT(dof_damping, tof(B.f("dof_damping")));
+  PUT(dof_frictionloss, tof(floss)); PUT(dof_invweight0, tof(B.f("dof_invweight0")));
+  PUT(dof_solref, tof(B.f("dof_solref"))); PUT(dof_solimp, tof(B.f("dof_solimp")));
 
   // compact collidable geoms
   std::vector<int> gtype = B.i("geom_type"), gcon = B.i("geom_contype"), gaff = B.i("geom_conaffinity"),
@@ -669,11 +669,11 @@ static int build_model(const Blob& B, DModel& m, Packer& P) {
   }
   m.ngeom = (int)ctype.size();
   if (m.ngeom > MAXG) return fail(AW_EUNSUPPORTED, "too many collidable geoms");
-  P.add(&m.geom_type, ctype); P.add(&m.geom_bodyid, cbody); P.add(&m.geom_pos, cpos);
-  P.add(&m.geom_quat, cquat); P.add(&m.geom_size, csize); P.add(&m.geom_rbound, crb);
+  PUT(geom_type, ctype); PUT(geom_bodyid, cbody); PUT(geom_pos, cpos);
+  PUT(geom_quat, cquat); PUT(geom_size, csize); PUT(geom_rbound, crb);
 
-  P.add(&m.site_bodyid, B.i("site_bodyid")); P.add(&m.site_pos, tof(B.f("site_pos")));
-  P.add(&m.site_quat, tof(B.f("site_quat")));
+  PUT(site_bodyid, B.i("site_bodyid")); PUT(site_pos, tof(B.f("site_pos")));
+  PUT(site_quat, tof(B.f("site_quat")));
 
   // tendons: fixed, <= 2 joints
   std::vector<int> tadr = B.i("tendon_adr"), tnum = B.i("tendon_num"), wj = B.i("wrap_jnt");
@@ -686,18 +686,18 @@ static int build_model(const Blob& B, DModel& m, Packer& P) {
     d0[t] = wj[tadr[t]]; c0[t] = (float)wc[tadr[t]];
     d1[t] = tnum[t] > 1 ? wj[tadr[t] + 1] : -1; c1[t] = tnum[t] > 1 ? (float)wc[tadr[t] + 1] : 0.f;
   }
-  P.add(&m.ten_d0, d0); P.add(&m.ten_d1, d1); P.add(&m.ten_limited, B.i("tendon_limited"));
-  P.add(&m.ten_c0, c0); P.add(&m.ten_c1, c1); P.add(&m.ten_range, tof(B.f("tendon_range")));
-  P.add(&m.ten_margin, tof(B.f("tendon_margin"))); P.add(&m.ten_solref, tof(B.f("tendon_solref")));
-  P.add(&m.ten_solimp, tof(B.f("tendon_solimp"))); P.add(&m.ten_invweight0, tof(B.f("tendon_invweight0")));
+  PUT(ten_d0, d0); PUT(ten_d1, d1); PUT(ten_limited, B.i("tendon_limited"));
+  PUT(ten_c0, c0); PUT(ten_c1, c1); PUT(ten_range, tof(B.f("tendon_range")));
+  PUT(ten_margin, tof(B.f("tendon_margin"))); PUT(ten_solref, tof(B.f("tendon_solref")));
+  PUT(ten_solimp, tof(B.f("tendon_solimp"))); PUT(ten_invweight0, tof(B.f("tendon_invweight0")));
 
   std::vector<double> gain = B.f("actuator_gainprm");
   std::vector<float> g0(nu);
   for (int u = 0; u < nu; u++) g0[u] = (float)gain[3 * u];
-  P.add(&m.act_ctrllimited, B.i("actuator_ctrllimited")); P.add(&m.act_forcelimited, B.i("actuator_forcelimited"));
-  P.add(&m.act_gear, tof(B.f("actuator_gear"))); P.add(&m.act_gain, g0);
-  P.add(&m.act_bias, tof(B.f("actuator_biasprm"))); P.add(&m.act_ctrlrange, tof(B.f("actuator_ctrlrange")));
-  P.add(&m.act_forcerange, tof(B.f("actuator_forcerange")));
+  PUT(act_ctrllimited, B.i("actuator_ctrllimited")); PUT(act_forcelimited, B.i("actuator_forcelimited"));
+  PUT(act_gear, tof(B.f("actuator_gear"))); PUT(act_gain, g0);
+  PUT(act_bias, tof(B.f("actuator_biasprm"))); PUT(act_ctrlrange, tof(B.f("actuator_ctrlrange")));
+  PUT(act_forcerange, tof(B.f("actuator_forcerange")));
 
   // unified pair list: explicit pairs (own params), then candidates (params mixed here in fp64,
   // mj_contactParam with equal priorities)
@@ -758,10 +758,10 @@ static int build_model(const Blob& B, DModel& m, Packer& P) {
     m.cls_start[0] = 0;
     for (int c = 0; c < NCLASS; c++) m.cls_start[c + 1] = m.cls_start[c] + ccount[c];
     if (m.npairall > MAXDENSE * VS * 2) return fail(AW_EUNSUPPORTED, "too many collision pairs");
-    P.add(&m.cp_class, pcls); P.add(&m.cp_rb, prb);
+    PUT(cp_class, pcls); PUT(cp_rb, prb);
   }
-  P.add(&m.cp_g1, pg1); P.add(&m.cp_g2, pg2); P.add(&m.cp_condim, pcd); P.add(&m.cp_friction, pfr);
-  P.add(&m.cp_solref, psr); P.add(&m.cp_solimp, psi); P.add(&m.cp_margin, pmg); P.add(&m.cp_gap, pgp);
+  PUT(cp_g1, pg1); PUT(cp_g2, pg2); PUT(cp_condim, pcd); PUT(cp_friction, pfr);
+  PUT(cp_solref, psr); PUT(cp_solimp, psi); PUT(cp_margin, pmg); PUT(cp_gap, pgp);
 
   // task block
   std::vector<int> tidx = B.i("task_idx"), pf = B.i("task_param_field"), po = B.i("task_param_obj"),
@@ -785,7 +785,7 @@ static int build_model(const Blob& B, DModel& m, Packer& P) {
       }
   }
   m.ntouch = (int)ts.size();
-  P.add(&m.touch_site, ts); P.add(&m.touch_adr, ts); P.add(&m.touch_type, ttype); P.add(&m.touch_size, tsize);
+  PUT(touch_site, ts); PUT(touch_adr, ts); PUT(touch_type, ttype); PUT(touch_size, tsize);
   {
     // per-object "some parameter overrides this" flags (kinematics applies those overrides inline)
     std::vector<int> bo(nbody, 0), so(std::max(nsite, 1), 0), go(std::max(m.ngeom, 1), 0);
@@ -794,15 +794,15 @@ static int build_model(const Blob& B, DModel& m, Packer& P) {
       else if (pf[p] == 2) so[po[p]] = 1;
       else if (pf[p] == 4 || pf[p] == 5) go[po[p]] = 1;
     }
-    P.add(&m.body_ovr, bo); P.add(&m.site_ovr, so); P.add(&m.geom_ovr, go);
+    PUT(body_ovr, bo); PUT(site_ovr, so); PUT(geom_ovr, go);
   }
-  P.add(&m.task_idx, tidx); P.add(&m.param_field, pf); P.add(&m.param_obj, po); P.add(&m.param_comp, pc);
-  P.add(&m.act_mid, tof(B.f("task_act_mid"))); P.add(&m.act_rng, tof(B.f("task_act_rng")));
-  P.add(&m.param_default, tof(B.f("task_param_default")));
+  PUT(task_idx, tidx); PUT(param_field, pf); PUT(param_obj, po); PUT(param_comp, pc);
+  PUT(act_mid, tof(B.f("task_act_mid"))); PUT(act_rng, tof(B.f("task_act_rng")));
+  PUT(param_default, tof(B.f("task_param_default")));
   std::vector<double> dlo = B.f("task_draw_lo"), dhi = B.f("task_draw_hi");
   m.ndraw = (int)dlo.size();
   if (m.ndraw > 8) return fail(AW_EUNSUPPORTED, "too many reset draws");
-  P.add(&m.draw_lo, tof(dlo)); P.add(&m.draw_hi, tof(dhi));
+  PUT(draw_lo, tof(dlo)); PUT(draw_hi, tof(dhi));
   return AW_OK;
 }
 
@@ -853,15 +853,15 @@ int aw_create(const void* blob, size_t nbytes, int n_envs, int device, aw_handle
   aw_handle* h = new aw_handle();
   h->device = device;
   h->nenv = n_envs;
-  Packer P;
-  int rc = build_model(B, h->m, P);
+  std::unique_ptr<MData> md(new MData());   // value-initialised: zero
+  int rc = build_model(B, h->m, *md);
   if (rc) { delete h; return rc; }
   h->NV = h->m.nv;
   if (h->NV != 30 && h->NV != 33 && h->NV != 36) { delete h; return fail(AW_EUNSUPPORTED, "nv not instantiated"); }
   HIPCHK(hipSetDevice(device));
-  HIPCHK(hipMalloc(&h->dmodel, P.buf.size()));
-  HIPCHK(hipMemcpy(h->dmodel, P.buf.data(), P.buf.size(), hipMemcpyHostToDevice));
-  for (auto& f : P.fix) *f.second = (const char*)h->dmodel + f.first;
+  HIPCHK(hipMalloc(&h->dmodel, sizeof(MData)));
+  HIPCHK(hipMemcpy(h->dmodel, md.get(), sizeof(MData), hipMemcpyHostToDevice));
+  h->m.d = (const MData*)h->dmodel;
   // state
   size_t N = (size_t)n_envs, nq = h->m.nq, nv = h->m.nv, np = std::max(h->m.nparam, 1);
   size_t bytes = N * (nq + 2 * nv + np) * 4 + N * 4 * 10 + 256;

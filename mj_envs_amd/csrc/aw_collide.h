@@ -708,15 +708,15 @@ AW_DEV void c_convex(const DModel& m, const GV& a, const GV& b, float margin, Em
 
 // ---------------------------------------------------------------------------------------
 AW_DEV void collide_pair(const DModel& m, Env& s, int pair) {
-  int g1 = m.cp_g1[pair], g2 = m.cp_g2[pair];
+  int g1 = MD(cp_g1, pair), g2 = MD(cp_g2, pair);
   GV a, b;
-  a.type = m.geom_type[g1];
-  b.type = m.geom_type[g2];
+  a.type = MD(geom_type, g1);
+  b.type = MD(geom_type, g2);
   for (int k = 0; k < 3; k++) {
     a.pos[k] = s.gxpos[g1][k]; b.pos[k] = s.gxpos[g2][k];
     a.size[k] = s.gsize[g1][k]; b.size[k] = s.gsize[g2][k];
   }
-  float margin = m.cp_margin[pair];   // the bounding-sphere test ran in the broadphase
+  float margin = MD(cp_margin, pair);   // the bounding-sphere test ran in the broadphase
   {
     float q1[4], q2[4];
     for (int k = 0; k < 4; k++) { q1[k] = s.gxquat[g1][k]; q2[k] = s.gxquat[g2][k]; }

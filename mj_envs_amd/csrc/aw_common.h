@@ -83,7 +83,65 @@ enum {
 enum { ST_BADQPOS = 1, ST_BADQVEL = 2, ST_BADQACC = 4, ST_CON_OVERFLOW = 8, ST_EFC_OVERFLOW = 16 };
 
 // ---------------------------------------------------------------------------------------
-// Device model: flat fp32/int32 arrays in one HBM allocation (built on the host from the blob).
+// Device model.  Every per-object array sits at a compile-time offset inside ONE read-only
+// table (MData, fixed capacities), so a kernel holds a single uniform base pointer and each
+// model read is base + constant + 32-bit lane offset.  (One pointer per array made the
+// compiler keep ~100 per-lane 64-bit addresses live across a substep -- spills.)
+constexpr int MAXPAIR = 320;  // explicit pairs + broadphase candidates
+constexpr int MAXTIDX = 16;   // task object ids
+
+#define AW_MODEL_ARRAYS(X)                                                                     \
+  X(int, body_parentid, MAXB) X(int, body_rootid, MAXB) X(int, body_dofnum, MAXB)               \
+  X(int, body_dofadr, MAXB) X(int, body_subtree_end, MAXB) X(int, level_start, MAXLEV + 1)      \
+  X(int, level_body, MAXB) X(float, body_pos, MAXB * 3) X(float, body_quat, MAXB * 4)           \
+  X(float, body_ipos, MAXB * 3) X(float, body_iquat, MAXB * 4) X(float, body_mass, MAXB)        \
+  X(float, body_inertia, MAXB * 3) X(float, body_invweight0, MAXB * 2)                          \
+  X(float, body_subtreemass, MAXB)                                                             \
+  X(unsigned long long, body_dofmask, MAXB) /* dofs moving the body (ancestor chain) */        \
+  X(int, jnt_type, MAXV) X(int, jnt_bodyid, MAXV) X(int, jnt_limited, MAXV)                     \
+  X(float, jnt_pos, MAXV * 3) X(float, jnt_axis, MAXV * 3) X(float, jnt_range, MAXV * 2)        \
+  X(float, jnt_margin, MAXV) X(float, jnt_solref, MAXV * 2) X(float, jnt_solimp, MAXV * 5)      \
+  X(int, dof_bodyid, MAXV) X(int, dof_act, MAXV) /* actuator driving the dof or -1 */          \
+  X(int, fl_dof, MAXV) X(int, fl_row, MAXV) /* frictionloss row r -> dof, dof -> row / -1 */   \
+  X(unsigned long long, dof_ancmask, MAXV) /* strict ancestor dofs */                          \
+  X(float, dof_armature, MAXV) X(float, dof_damping, MAXV) X(float, dof_frictionloss, MAXV)     \
+  X(float, dof_invweight0, MAXV) X(float, dof_solref, MAXV * 2) X(float, dof_solimp, MAXV * 5)  \
+  X(int, geom_type, MAXG) X(int, geom_bodyid, MAXG) X(float, geom_pos, MAXG * 3)                \
+  X(float, geom_quat, MAXG * 4) X(float, geom_size, MAXG * 3) X(float, geom_rbound, MAXG)       \
+  X(int, site_bodyid, MAXS) X(float, site_pos, MAXS * 3) X(float, site_quat, MAXS * 4)          \
+  X(int, touch_site, MAXTOUCH) X(int, touch_adr, MAXTOUCH) X(int, touch_type, MAXTOUCH)         \
+  X(float, touch_size, MAXTOUCH * 3)                                                           \
+  X(int, ten_d0, MAXT) X(int, ten_d1, MAXT) X(int, ten_limited, MAXT) X(float, ten_c0, MAXT)    \
+  X(float, ten_c1, MAXT) X(float, ten_range, MAXT * 2) X(float, ten_margin, MAXT)               \
+  X(float, ten_solref, MAXT * 2) X(float, ten_solimp, MAXT * 5) X(float, ten_invweight0, MAXT)  \
+  X(int, act_ctrllimited, MAXU) X(int, act_forcelimited, MAXU) X(float, act_gear, MAXU)         \
+  X(float, act_gain, MAXU) X(float, act_bias, MAXU * 3) X(float, act_ctrlrange, MAXU * 2)       \
+  X(float, act_forcerange, MAXU * 2)                                                           \
+  /* explicit pairs first, then dynamic candidates; params pre-mixed on the host */           \
+  X(int, cp_g1, MAXPAIR) X(int, cp_g2, MAXPAIR) X(int, cp_condim, MAXPAIR)                      \
+  X(float, cp_friction, MAXPAIR * 5) X(float, cp_solref, MAXPAIR * 2)                           \
+  X(float, cp_solimp, MAXPAIR * 5) X(float, cp_margin, MAXPAIR) X(float, cp_gap, MAXPAIR)       \
+  /* broadphase: collider class of each pair, bounding radius sum (< 0: plane pair) */        \
+  X(int, cp_class, MAXPAIR) X(float, cp_rb, MAXPAIR)                                           \
+  X(int, body_ovr, MAXB) X(int, site_ovr, MAXS) X(int, geom_ovr, MAXG) /* 1: overridden */    \
+  X(int, task_idx, MAXTIDX) X(int, param_field, MAXP) X(int, param_obj, MAXP)                   \
+  X(int, param_comp, MAXP) X(float, act_mid, MAXU) X(float, act_rng, MAXU)                      \
+  X(float, param_default, MAXP) X(float, draw_lo, 8) X(float, draw_hi, 8)
+
+struct MData {
+#define AW_X(T, name, n) T name[n];
+  AW_MODEL_ARRAYS(AW_X)
+#undef AW_X
+};
+
+// model read: uniform table base + zero-extended 32-bit byte offset, which maps onto the
+// global_load saddr form (SGPR base, one VGPR offset) instead of a 64-bit per-lane address
+template <class T>
+AW_DEV T mld(const T* base, unsigned i) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + i * (unsigned)sizeof(T));
+}
+#define MD(name, idx) ::aw::mld(m.d->name, (unsigned)(idx))
+
 struct DModel {
   int nq, nv, nu, nbody, njnt, ngeom, nsite, ntendon, npairall, nlevel;
   int nfl;                // dofs with frictionloss (rows 0..nfl-1 are these, in dof order)
@@ -93,51 +151,8 @@ struct DModel {
   int iterations, noslip_iterations, mpr_iterations, disableflags;
   float timestep, gravity[3], tolerance, noslip_tolerance, mpr_tolerance, meaninertia;
   float pen_length, tar_length;
-
-  const int* body_parentid; const int* body_rootid; const int* body_dofnum; const int* body_dofadr;
-  const int* body_subtree_end; const int* level_start; const int* level_body;
-  const float* body_pos; const float* body_quat; const float* body_ipos; const float* body_iquat;
-  const float* body_mass; const float* body_inertia; const float* body_invweight0;
-  const float* body_subtreemass;
-  const unsigned long long* body_dofmask;  // dofs moving the body (ancestor chain)
-
-  const int* jnt_type; const int* jnt_bodyid; const int* jnt_limited;
-  const float* jnt_pos; const float* jnt_axis; const float* jnt_range; const float* jnt_margin;
-  const float* jnt_solref; const float* jnt_solimp;
-
-  const int* dof_bodyid; const int* dof_act;  // actuator driving the dof or -1
-  const int* fl_dof; const int* fl_row;       // frictionloss row r -> dof, dof -> row (or -1)
-  const unsigned long long* dof_ancmask;      // strict ancestor dofs
-  const float* dof_armature; const float* dof_damping; const float* dof_frictionloss;
-  const float* dof_invweight0; const float* dof_solref; const float* dof_solimp;
-
-  const int* geom_type; const int* geom_bodyid;
-  const float* geom_pos; const float* geom_quat; const float* geom_size; const float* geom_rbound;
-
-  const int* site_bodyid; const float* site_pos; const float* site_quat;
-  const int* touch_site; const int* touch_adr; const int* touch_type; const float* touch_size;
-
-  const int* ten_d0; const int* ten_d1; const int* ten_limited;
-  const float* ten_c0; const float* ten_c1; const float* ten_range; const float* ten_margin;
-  const float* ten_solref; const float* ten_solimp; const float* ten_invweight0;
-
-  const int* act_ctrllimited; const int* act_forcelimited;
-  const float* act_gear; const float* act_gain; const float* act_bias; const float* act_ctrlrange;
-  const float* act_forcerange;
-
-  // explicit pairs first, then dynamic candidates; params pre-mixed on the host
-  const int* cp_g1; const int* cp_g2; const int* cp_condim;
-  const float* cp_friction; const float* cp_solref; const float* cp_solimp; const float* cp_margin;
-  const float* cp_gap;
-  // broadphase: collider class of each pair (narrowphase is run class-major after compaction),
-  // bounding-sphere radius sum rbound1 + rbound2 + margin (< 0: plane pair, always tested)
-  const int* cp_class; const float* cp_rb;
-  int cls_start[NCLASS + 1];  // class c owns list slots [cls_start[c], cls_start[c+1])
-
-  const int* body_ovr; const int* site_ovr; const int* geom_ovr;   // 1: some param overrides it
-  const int* task_idx; const int* param_field; const int* param_obj; const int* param_comp;
-  const float* act_mid; const float* act_rng; const float* param_default;
-  const float* draw_lo; const float* draw_hi;
+  int cls_start[NCLASS + 1];  // collider class c owns pair-list slots [cls_start[c], cls_start[c+1])
+  const MData* __restrict__ d;
 };
 
 // ---------------------------------------------------------------------------------------

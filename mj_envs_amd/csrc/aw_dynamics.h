@@ -14,16 +14,16 @@ namespace aw {
 // (geom_size: every collider; body_mass: subtree sums); other overrides are applied where
 // the field is read (apply_ovr)
 AW_DEV void stage_model(const DModel& m, Env& s, const float* params, int lane) {
-  if (lane < m.nparam) s.prm[lane] = params ? params[lane] : m.param_default[lane];
-  for (int b = lane; b < m.nbody; b += 64) s.bmass[b] = m.body_mass[b];
+  if (lane < m.nparam) s.prm[lane] = params ? params[lane] : MD(param_default, lane);
+  for (int b = lane; b < m.nbody; b += 64) s.bmass[b] = MD(body_mass, b);
   for (int g = lane; g < m.ngeom; g += 64)
-    for (int k = 0; k < 3; k++) s.gsize[g][k] = m.geom_size[3 * g + k];
+    for (int k = 0; k < 3; k++) s.gsize[g][k] = MD(geom_size, 3 * g + k);
   wsync();
   if (lane == 0) {
     for (int p = 0; p < m.nparam; p++) {
-      int o = m.param_obj[p], c = m.param_comp[p];
-      if (m.param_field[p] == 3) s.bmass[o] = s.prm[p];
-      else if (m.param_field[p] == 5) s.gsize[o][c] = s.prm[p];
+      int o = MD(param_obj, p), c = MD(param_comp, p);
+      if (MD(param_field, p) == 3) s.bmass[o] = s.prm[p];
+      else if (MD(param_field, p) == 5) s.gsize[o][c] = s.prm[p];
     }
   }
   wsync();
@@ -32,8 +32,8 @@ AW_DEV void stage_model(const DModel& m, Env& s, const float* params, int lane) 
 template <int N>
 AW_DEV void apply_ovr(const DModel& m, const Env& s, int field, int obj, float (&v)[N]) {
   for (int p = 0; p < m.nparam; p++)
-    if (m.param_field[p] == field && m.param_obj[p] == obj) {
-      const int c = m.param_comp[p];
+    if (MD(param_field, p) == field && MD(param_obj, p) == obj) {
+      const int c = MD(param_comp, p);
       const float x = s.prm[p];
 #pragma unroll
       for (int k = 0; k < N; k++) v[k] = k == c ? x : v[k];
@@ -49,26 +49,26 @@ AW_DEV void stage_kinematics(const DModel& m, Env& s, int lane) {
   }
   wsync();
   for (int lev = 1; lev < m.nlevel; lev++) {
-    int beg = m.level_start[lev], end = m.level_start[lev + 1];
+    int beg = MD(level_start, lev), end = MD(level_start, lev + 1);
     for (int idx = beg + lane; idx < end; idx += 64) {
-      int b = m.level_body[idx], p = m.body_parentid[b];
+      int b = MD(level_body, idx), p = MD(body_parentid, b);
       float xp[3], xq[4], bp[3], bq[4], pq[4];
-      for (int k = 0; k < 3; k++) bp[k] = m.body_pos[3 * b + k];
-      for (int k = 0; k < 4; k++) { bq[k] = m.body_quat[4 * b + k]; pq[k] = s.xquat[p][k]; }
-      if (m.body_ovr[b]) { apply_ovr<3>(m, s, 0, b, bp); apply_ovr<4>(m, s, 1, b, bq); }
+      for (int k = 0; k < 3; k++) bp[k] = MD(body_pos, 3 * b + k);
+      for (int k = 0; k < 4; k++) { bq[k] = MD(body_quat, 4 * b + k); pq[k] = s.xquat[p][k]; }
+      if (MD(body_ovr, b)) { apply_ovr<3>(m, s, 0, b, bp); apply_ovr<4>(m, s, 1, b, bq); }
       rotvq(xp, bp, pq);
       add3(xp, xp, s.xpos[p]);
       mulq(xq, pq, bq);
-      int da = m.body_dofadr[b];
-      for (int k = 0; k < m.body_dofnum[b]; k++) {
+      int da = MD(body_dofadr, b);
+      for (int k = 0; k < MD(body_dofnum, b); k++) {
         int j = da + k;
         float axis[3], xaxis[3], xanchor[3], jp[3];
-        for (int q = 0; q < 3; q++) { axis[q] = m.jnt_axis[3 * j + q]; jp[q] = m.jnt_pos[3 * j + q]; }
+        for (int q = 0; q < 3; q++) { axis[q] = MD(jnt_axis, 3 * j + q); jp[q] = MD(jnt_pos, 3 * j + q); }
         rotvq(xaxis, axis, xq);
         rotvq(xanchor, jp, xq);
         add3(xanchor, xanchor, xp);
         float q = s.qpos[j];
-        if (m.jnt_type[j] == JNT_SLIDE) {
+        if (MD(jnt_type, j) == JNT_SLIDE) {
           for (int c = 0; c < 3; c++) xp[c] += xaxis[c] * q;
         } else {
           float sn, cs, ql[4], v[3];
@@ -90,35 +90,35 @@ AW_DEV void stage_kinematics(const DModel& m, Env& s, int lane) {
   }
   // geoms (compact collidable list), sites, inertial frames
   for (int g = lane; g < m.ngeom; g += 64) {
-    int b = m.geom_bodyid[g];
+    int b = MD(geom_bodyid, g);
     float v[3], q[4], gq[4], gp[3], bq[4];
-    for (int c = 0; c < 3; c++) gp[c] = m.geom_pos[3 * g + c];
-    if (m.geom_ovr[g]) apply_ovr<3>(m, s, 4, g, gp);
-    for (int c = 0; c < 4; c++) { gq[c] = m.geom_quat[4 * g + c]; bq[c] = s.xquat[b][c]; }
+    for (int c = 0; c < 3; c++) gp[c] = MD(geom_pos, 3 * g + c);
+    if (MD(geom_ovr, g)) apply_ovr<3>(m, s, 4, g, gp);
+    for (int c = 0; c < 4; c++) { gq[c] = MD(geom_quat, 4 * g + c); bq[c] = s.xquat[b][c]; }
     rotvq(v, gp, bq);
     add3(s.gxpos[g], v, s.xpos[b]);
     mulq(q, bq, gq);
     for (int c = 0; c < 4; c++) s.gxquat[g][c] = q[c];
   }
   for (int i = lane; i < m.nsite; i += 64) {
-    int b = m.site_bodyid[i];
+    int b = MD(site_bodyid, i);
     float v[3], sp[3], bq[4];
-    for (int c = 0; c < 3; c++) sp[c] = m.site_pos[3 * i + c];
-    if (m.site_ovr[i]) apply_ovr<3>(m, s, 2, i, sp);
+    for (int c = 0; c < 3; c++) sp[c] = MD(site_pos, 3 * i + c);
+    if (MD(site_ovr, i)) apply_ovr<3>(m, s, 2, i, sp);
     for (int c = 0; c < 4; c++) bq[c] = s.xquat[b][c];
     rotvq(v, sp, bq);
     add3(s.sxpos[i], v, s.xpos[b]);
   }
   if (lane < m.ntouch) {
-    int i = m.touch_site[lane], b = m.site_bodyid[i];
+    int i = MD(touch_site, lane), b = MD(site_bodyid, i);
     float q[4], sq[4];
-    for (int c = 0; c < 4; c++) sq[c] = m.site_quat[4 * i + c];
+    for (int c = 0; c < 4; c++) sq[c] = MD(site_quat, 4 * i + c);
     mulq(q, s.xquat[b], sq);
     q2m(s.txmat[lane], q);
   }
   for (int b = lane; b < m.nbody; b += 64) {
     float v[3], ip[3], bq[4];
-    for (int c = 0; c < 3; c++) ip[c] = m.body_ipos[3 * b + c];
+    for (int c = 0; c < 3; c++) ip[c] = MD(body_ipos, 3 * b + c);
     for (int c = 0; c < 4; c++) bq[c] = s.xquat[b][c];
     rotvq(v, ip, bq);
     add3(s.xipos[b], v, s.xpos[b]);
@@ -130,11 +130,11 @@ AW_DEV void stage_kinematics(const DModel& m, Env& s, int lane) {
 AW_DEV void stage_com(const DModel& m, Env& s, int lane) {
   for (int b = lane; b < m.nbody; b += 64) {
     float acc[3] = {0, 0, 0};
-    for (int d = b; d < m.body_subtree_end[b]; d++) {
+    for (int d = b; d < MD(body_subtree_end, b); d++) {
       float md = s.bmass[d];
       acc[0] += md * s.xipos[d][0]; acc[1] += md * s.xipos[d][1]; acc[2] += md * s.xipos[d][2];
     }
-    float stm = m.body_subtreemass[b];
+    float stm = MD(body_subtreemass, b);
     if (stm < MINVAL) copy3(s.subcom[b], s.xipos[b]);
     else scl3(s.subcom[b], acc, 1.0f / stm);
   }
@@ -143,12 +143,12 @@ AW_DEV void stage_com(const DModel& m, Env& s, int lane) {
     float* c = s.cinert[b];
     if (b == 0) { for (int k = 0; k < 10; k++) c[k] = 0; continue; }
     float q[4], iq[4], R[9], dif[3];
-    for (int k = 0; k < 4; k++) iq[k] = m.body_iquat[4 * b + k];
+    for (int k = 0; k < 4; k++) iq[k] = MD(body_iquat, 4 * b + k);
     mulq(q, s.xquat[b], iq);
     q2m(R, q);
-    const float* I = &m.body_inertia[3 * b];
+    const float* I = &m.d->body_inertia[3 * b];
     float mass = s.bmass[b];
-    sub3(dif, s.xipos[b], s.subcom[m.body_rootid[b]]);
+    sub3(dif, s.xipos[b], s.subcom[MD(body_rootid, b)]);
     float T[9];
     for (int a = 0; a < 3; a++)
       for (int bb = 0; bb < 3; bb++)
@@ -163,15 +163,15 @@ AW_DEV void stage_com(const DModel& m, Env& s, int lane) {
     c[9] = mass;
   }
   if (lane < m.nv) {
-    int j = lane, b = m.dof_bodyid[j];
+    int j = lane, b = MD(dof_bodyid, j);
     float* cd = s.cdof[j];
     const float* axis = s.xaxis[j];
-    if (m.jnt_type[j] == JNT_SLIDE) {
+    if (MD(jnt_type, j) == JNT_SLIDE) {
       cd[0] = cd[1] = cd[2] = 0;
       copy3(cd + 3, axis);
     } else {
       float off[3];
-      sub3(off, s.subcom[m.body_rootid[b]], s.xanchor[j]);
+      sub3(off, s.subcom[MD(body_rootid, b)], s.xanchor[j]);
       copy3(cd, axis);
       cross3(cd + 3, axis, off);
     }
@@ -188,7 +188,7 @@ AW_DEV void stage_crb(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
   for (int k = 0; k < 10; k++) acc[k] = 0;
   const int bb = lane < m.nbody ? lane : 0;
   if (lane < m.nbody && lane > 0)
-    for (int d = bb; d < m.body_subtree_end[bb]; d++)
+    for (int d = bb; d < MD(body_subtree_end, bb); d++)
       for (int k = 0; k < 10; k++) acc[k] += s.cinert[d][k];
   wsync();
   if (lane < m.nbody)
@@ -197,16 +197,16 @@ AW_DEV void stage_crb(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
   const int li = lane < NV ? lane : NV - 1;
   float ci[6], bi[6];
   for (int k = 0; k < 6; k++) ci[k] = s.cdof[li][k];
-  mul_inert_vec(bi, s.cinert[m.dof_bodyid[li]], ci);
+  mul_inert_vec(bi, s.cinert[MD(dof_bodyid, li)], ci);
   for (int k = 0; k < 6; k++) s.buf[li][k] = bi[k];
   wsync();
-  const unsigned long long anc = m.dof_ancmask[li];
-  const float arm = m.dof_armature[li];
+  const unsigned long long anc = MD(dof_ancmask, li);
+  const float arm = MD(dof_armature, li);
 #pragma unroll
   for (int k = 0; k < NV; k++) {
     float ck[6], bk[6];
     for (int c = 0; c < 6; c++) { ck[c] = s.cdof[k][c]; bk[c] = s.buf[k][c]; }
-    const unsigned long long anck = m.dof_ancmask[k];
+    const unsigned long long anck = MD(dof_ancmask, k);
     float v;
     if (k == li) v = dot6(ci, bi) + arm;
     else if ((anc >> k) & 1ull) v = dot6(ck, bi);
@@ -227,13 +227,13 @@ AW_DEV float stage_velocity(const DModel& m, Env& s, int lane) {
   }
   wsync();
   for (int lev = 1; lev < m.nlevel; lev++) {
-    int beg = m.level_start[lev], end = m.level_start[lev + 1];
+    int beg = MD(level_start, lev), end = MD(level_start, lev + 1);
     for (int idx = beg + lane; idx < end; idx += 64) {
-      int b = m.level_body[idx], p = m.body_parentid[b];
+      int b = MD(level_body, idx), p = MD(body_parentid, b);
       float cv[6], ca[6];
       for (int k = 0; k < 6; k++) { cv[k] = cvel[p][k]; ca[k] = cacc[p][k]; }
-      int da = m.body_dofadr[b];
-      for (int q = 0; q < m.body_dofnum[b]; q++) {
+      int da = MD(body_dofadr, b);
+      for (int q = 0; q < MD(body_dofnum, b); q++) {
         int j = da + q;
         float cd[6], cdd[6], qv = s.qvel[j];
         for (int k = 0; k < 6; k++) cd[k] = s.cdof[j][k];
@@ -260,7 +260,7 @@ AW_DEV float stage_velocity(const DModel& m, Env& s, int lane) {
   const int bb = lane < m.nbody ? lane : 0;
   for (int k = 0; k < 6; k++) sub[k] = 0;
   if (lane < m.nbody && lane > 0)
-    for (int d = bb; d < m.body_subtree_end[bb]; d++)
+    for (int d = bb; d < MD(body_subtree_end, bb); d++)
       for (int k = 0; k < 6; k++) sub[k] += cacc[d][k];
   wsync();
   if (lane < m.nbody)
@@ -269,19 +269,19 @@ AW_DEV float stage_velocity(const DModel& m, Env& s, int lane) {
   float qfrc = 0.f;
   if (lane < m.nv) {
     int j = lane;
-    float bias = dot6(s.cdof[j], cvel[m.dof_bodyid[j]]);
-    float pas = (m.disableflags & DSBL_PASSIVE) ? 0.f : -m.dof_damping[j] * s.qvel[j];
+    float bias = dot6(s.cdof[j], cvel[MD(dof_bodyid, j)]);
+    float pas = (m.disableflags & DSBL_PASSIVE) ? 0.f : -MD(dof_damping, j) * s.qvel[j];
     float act = 0.f;
-    int u = m.dof_act[j];
+    int u = MD(dof_act, j);
     if (u >= 0 && !(m.disableflags & DSBL_ACTUATION)) {
       float ctrl = s.ctrl[u];
-      if (m.act_ctrllimited[u] && !(m.disableflags & DSBL_CLAMPCTRL))
-        ctrl = clampf(ctrl, m.act_ctrlrange[2 * u], m.act_ctrlrange[2 * u + 1]);
-      float gear = m.act_gear[u];
+      if (MD(act_ctrllimited, u) && !(m.disableflags & DSBL_CLAMPCTRL))
+        ctrl = clampf(ctrl, MD(act_ctrlrange, 2 * u), MD(act_ctrlrange, 2 * u + 1));
+      float gear = MD(act_gear, u);
       float len = gear * s.qpos[j], vel = gear * s.qvel[j];
-      const float* bp = &m.act_bias[3 * u];
-      float f = m.act_gain[u] * ctrl + bp[0] + bp[1] * len + bp[2] * vel;
-      if (m.act_forcelimited[u]) f = clampf(f, m.act_forcerange[2 * u], m.act_forcerange[2 * u + 1]);
+      const float* bp = &m.d->act_bias[3 * u];
+      float f = MD(act_gain, u) * ctrl + bp[0] + bp[1] * len + bp[2] * vel;
+      if (MD(act_forcelimited, u)) f = clampf(f, MD(act_forcerange, 2 * u), MD(act_forcerange, 2 * u + 1));
       act = gear * f;
     }
     qfrc = pas - bias + act;

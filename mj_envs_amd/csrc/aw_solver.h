@@ -143,20 +143,20 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
   const int nfl = (m.disableflags & DSBL_FRICTIONLOSS) ? 0 : m.nfl;
   // frictionloss rows (dof order)
   if (lane < nfl) {
-    int d = m.fl_dof[lane];
+    int d = MD(fl_dof, lane);
     s.efc_type[lane] = C_FRIC_DOF; s.efc_id[lane] = d;
     s.efc_i0[lane] = d; s.efc_i1[lane] = -1; s.efc_v0[lane] = 1.f; s.efc_v1[lane] = 0.f;
-    s.rowbuf[lane] = 0.f; s.efc_floss[lane] = m.dof_frictionloss[d]; s.efc_force[lane] = m.dof_invweight0[d];
+    s.rowbuf[lane] = 0.f; s.efc_floss[lane] = MD(dof_frictionloss, d); s.efc_force[lane] = MD(dof_invweight0, d);
   }
   // joint limits: lower then upper per joint, joints in order
   const bool lim = !(m.disableflags & DSBL_LIMIT);
   int lo = 0, hi = 0;
   float dlo = 0, dhi = 0, mg = 0;
-  if (lim && lane < m.njnt && m.jnt_limited[lane]) {
+  if (lim && lane < m.njnt && MD(jnt_limited, lane)) {
     float q = s.qpos[lane];
-    mg = m.jnt_margin[lane];
-    dlo = q - m.jnt_range[2 * lane];
-    dhi = m.jnt_range[2 * lane + 1] - q;
+    mg = MD(jnt_margin, lane);
+    dlo = q - MD(jnt_range, 2 * lane);
+    dhi = MD(jnt_range, 2 * lane + 1) - q;
     lo = dlo < mg; hi = dhi < mg;
   }
   int njl;
@@ -168,17 +168,17 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
       if (r >= MAXEFC) { atomicOr(&s.status, (unsigned)ST_EFC_OVERFLOW); continue; }
       s.efc_type[r] = C_LIM_JNT; s.efc_id[r] = lane;
       s.efc_i0[r] = lane; s.efc_i1[r] = -1; s.efc_v0[r] = side ? -1.f : 1.f; s.efc_v1[r] = 0.f;
-      s.rowbuf[r] = (side ? dhi : dlo) - mg; s.efc_floss[r] = 0.f; s.efc_force[r] = m.dof_invweight0[lane];
+      s.rowbuf[r] = (side ? dhi : dlo) - mg; s.efc_floss[r] = 0.f; s.efc_force[r] = MD(dof_invweight0, lane);
     }
   }
   // tendon limits
   lo = hi = 0;
-  if (lim && lane < m.ntendon && m.ten_limited[lane]) {
-    const int d1 = m.ten_d1[lane];
-    float len = m.ten_c0[lane] * s.qpos[m.ten_d0[lane]] + (d1 >= 0 ? m.ten_c1[lane] * s.qpos[d1] : 0.f);
-    mg = m.ten_margin[lane];
-    dlo = len - m.ten_range[2 * lane];
-    dhi = m.ten_range[2 * lane + 1] - len;
+  if (lim && lane < m.ntendon && MD(ten_limited, lane)) {
+    const int d1 = MD(ten_d1, lane);
+    float len = MD(ten_c0, lane) * s.qpos[MD(ten_d0, lane)] + (d1 >= 0 ? MD(ten_c1, lane) * s.qpos[d1] : 0.f);
+    mg = MD(ten_margin, lane);
+    dlo = len - MD(ten_range, 2 * lane);
+    dhi = MD(ten_range, 2 * lane + 1) - len;
     lo = dlo < mg; hi = dhi < mg;
   }
   int ntl;
@@ -190,9 +190,9 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
       if (r >= MAXEFC) { atomicOr(&s.status, (unsigned)ST_EFC_OVERFLOW); continue; }
       float sg = side ? -1.f : 1.f;
       s.efc_type[r] = C_LIM_TEN; s.efc_id[r] = lane;
-      s.efc_i0[r] = m.ten_d0[lane]; s.efc_i1[r] = m.ten_d1[lane];
-      s.efc_v0[r] = sg * m.ten_c0[lane]; s.efc_v1[r] = sg * m.ten_c1[lane];
-      s.rowbuf[r] = (side ? dhi : dlo) - mg; s.efc_floss[r] = 0.f; s.efc_force[r] = m.ten_invweight0[lane];
+      s.efc_i0[r] = MD(ten_d0, lane); s.efc_i1[r] = MD(ten_d1, lane);
+      s.efc_v0[r] = sg * MD(ten_c0, lane); s.efc_v1[r] = sg * MD(ten_c1, lane);
+      s.rowbuf[r] = (side ? dhi : dlo) - mg; s.efc_floss[r] = 0.f; s.efc_force[r] = MD(ten_invweight0, lane);
     }
   }
   int nsparse = nfl + njl + ntl;
@@ -202,7 +202,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
   int dim = 0, nr = 0, pair = 0;
   if (lane < ncon) {
     pair = s.con_pair[lane];
-    dim = m.cp_condim[pair];
+    dim = MD(cp_condim, pair);
     nr = dim == 1 ? 1 : 2 * (dim - 1);
   }
   int ntot;
@@ -216,18 +216,18 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
   if (lane < ncon && !inc) atomicOr(&s.status, (unsigned)ST_EFC_OVERFLOW);
   if (lane < ncon) s.con_efc[lane] = inc ? nsparse + doff : -1;
   if (inc) {
-    int g1 = m.cp_g1[pair], g2 = m.cp_g2[pair];
-    int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
-    float tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
-    float rot = m.body_invweight0[2 * b1 + 1] + m.body_invweight0[2 * b2 + 1];
-    float pm = s.con_dist[lane] - (m.cp_margin[pair] - m.cp_gap[pair]);
+    int g1 = MD(cp_g1, pair), g2 = MD(cp_g2, pair);
+    int b1 = MD(geom_bodyid, g1), b2 = MD(geom_bodyid, g2);
+    float tran = MD(body_invweight0, 2 * b1) + MD(body_invweight0, 2 * b2);
+    float rot = MD(body_invweight0, 2 * b1 + 1) + MD(body_invweight0, 2 * b2 + 1);
+    float pm = s.con_dist[lane] - (MD(cp_margin, pair) - MD(cp_gap, pair));
     int r = nsparse + doff;
     if (dim == 1) {
       s.efc_type[r] = C_CON_FRICTIONLESS; s.efc_id[r] = lane; s.rowbuf[r] = pm; s.efc_floss[r] = 0.f;
       s.efc_force[r] = tran; s.efc_i0[r] = 0; s.efc_i1[r] = 0;
     } else {
       for (int k = 1; k < dim; k++) {
-        float fri = m.cp_friction[5 * pair + k - 1];
+        float fri = MD(cp_friction, 5 * pair + k - 1);
         float dA = tran + fri * fri * (k < 3 ? tran : rot);
         for (int sd = 0; sd < 2; sd++) {
           s.efc_type[r] = C_CON_PYRAMIDAL; s.efc_id[r] = lane; s.rowbuf[r] = pm; s.efc_floss[r] = 0.f;
@@ -244,25 +244,25 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
     int r0 = s.con_efc[c];
     if (r0 < 0) break;
     int pr = s.con_pair[c];
-    int cdim = m.cp_condim[pr];
+    int cdim = MD(cp_condim, pr);
     if (lane < NV) {
       int k = lane;
-      int b1 = m.geom_bodyid[m.cp_g1[pr]], b2 = m.geom_bodyid[m.cp_g2[pr]];
+      int b1 = MD(geom_bodyid, MD(cp_g1, pr)), b2 = MD(geom_bodyid, MD(cp_g2, pr));
       const float* pos = s.con_pos[c];
       float fr[9];
       for (int q = 0; q < 3; q++) { fr[q] = s.con_nrm[c][q]; fr[3 + q] = 0.f; }
       make_frame(fr);
       const float* cd = s.cdof[k];
       float jp[3] = {0, 0, 0}, jr[3] = {0, 0, 0};
-      if ((m.body_dofmask[b2] >> k) & 1ull) {
+      if ((MD(body_dofmask, b2) >> k) & 1ull) {
         float off3[3], t[3];
-        sub3(off3, pos, s.subcom[m.body_rootid[b2]]);
+        sub3(off3, pos, s.subcom[MD(body_rootid, b2)]);
         cross3(t, cd, off3);
         for (int q = 0; q < 3; q++) { jr[q] += cd[q]; jp[q] += cd[3 + q] + t[q]; }
       }
-      if ((m.body_dofmask[b1] >> k) & 1ull) {
+      if ((MD(body_dofmask, b1) >> k) & 1ull) {
         float off3[3], t[3];
-        sub3(off3, pos, s.subcom[m.body_rootid[b1]]);
+        sub3(off3, pos, s.subcom[MD(body_rootid, b1)]);
         cross3(t, cd, off3);
         for (int q = 0; q < 3; q++) { jr[q] -= cd[q]; jp[q] -= cd[3 + q] + t[q]; }
       }
@@ -273,7 +273,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
         s.J[d][k] = B[0];
       } else {
         for (int kk = 1; kk < cdim; kk++) {
-          float fri = m.cp_friction[5 * pr + kk - 1];
+          float fri = MD(cp_friction, 5 * pr + kk - 1);
           s.J[d][k] = B[0] + fri * B[kk];
           s.J[d + 1][k] = B[0] - fri * B[kk];
           d += 2;
@@ -286,10 +286,10 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
   for (int r = lane; r < s.nefc; r += 64) {
     int t = s.efc_type[r], id = s.efc_id[r];
     const float *solref, *solimp;
-    if (t == C_FRIC_DOF) { solref = &m.dof_solref[2 * id]; solimp = &m.dof_solimp[5 * id]; }
-    else if (t == C_LIM_JNT) { solref = &m.jnt_solref[2 * id]; solimp = &m.jnt_solimp[5 * id]; }
-    else if (t == C_LIM_TEN) { solref = &m.ten_solref[2 * id]; solimp = &m.ten_solimp[5 * id]; }
-    else { int pr = s.con_pair[id]; solref = &m.cp_solref[2 * pr]; solimp = &m.cp_solimp[5 * pr]; }
+    if (t == C_FRIC_DOF) { solref = &m.d->dof_solref[2 * id]; solimp = &m.d->dof_solimp[5 * id]; }
+    else if (t == C_LIM_JNT) { solref = &m.d->jnt_solref[2 * id]; solimp = &m.d->jnt_solimp[5 * id]; }
+    else if (t == C_LIM_TEN) { solref = &m.d->ten_solref[2 * id]; solimp = &m.d->ten_solimp[5 * id]; }
+    else { int pr = s.con_pair[id]; solref = &m.d->cp_solref[2 * pr]; solimp = &m.d->cp_solimp[5 * pr]; }
     float pm = s.rowbuf[r];          // stashed by the row assembly above
     float imp = getimpedance(solimp, pm);
     float dmax = clampf(solimp[1], 0.0001f, 0.9999f);
@@ -567,7 +567,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
     float dg = 0.f;   // inv(M)[lane][lane]
 #pragma unroll
     for (int k = 0; k < NV; k++) dg = k == lane ? Mi[k] : dg;
-    const int row = lane < NV ? m.fl_row[lane] : -1;
+    const int row = lane < NV ? MD(fl_row, lane) : -1;
     const bool has = row >= 0 && row < nsparse;
     if (has) ffl = s.efc_force[row];
     fl_ok = use_fl && has && dg >= MINVAL;
@@ -663,7 +663,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
     if (impr * scale < m.noslip_tolerance) break;
   }
   AW_PROF(s, PR_NS_ITER);
-  if (lane < NV && m.fl_row[lane] >= 0 && m.fl_row[lane] < nsparse) s.efc_force[m.fl_row[lane]] = ffl;
+  if (lane < NV && MD(fl_row, lane) >= 0 && MD(fl_row, lane) < nsparse) s.efc_force[MD(fl_row, lane)] = ffl;
   if (lane < ndense) s.efc_force[nsparse + lane] = fd;
   wsync();
 }
@@ -728,13 +728,13 @@ AW_DEV float ray_geom(const float* pos, const float* mat, const float* size, con
 // touch sensors of the task (mj_sensorAcc, mjSENS_TOUCH)
 AW_DEV void stage_touch(const DModel& m, Env& s, int lane) {
   for (int t = 0; t < m.ntouch; t++) {
-    int site = m.touch_site[t], bid = m.site_bodyid[site];
+    int site = MD(touch_site, t), bid = MD(site_bodyid, site);
     float val = 0.f;
     if (lane < s.ncon && s.con_efc[lane] >= 0 && !(m.disableflags & DSBL_SENSOR)) {
       int pr = s.con_pair[lane];
-      int b1 = m.geom_bodyid[m.cp_g1[pr]], b2 = m.geom_bodyid[m.cp_g2[pr]];
+      int b1 = MD(geom_bodyid, MD(cp_g1, pr)), b2 = MD(geom_bodyid, MD(cp_g2, pr));
       if (bid == b1 || bid == b2) {
-        int adr = s.con_efc[lane], dim = m.cp_condim[pr];
+        int adr = s.con_efc[lane], dim = MD(cp_condim, pr);
         float fn = 0.f;
         if (dim == 1) fn = s.efc_force[adr];
         else for (int j = 0; j < 2 * (dim - 1); j++) fn += s.efc_force[adr + j];
@@ -743,7 +743,7 @@ AW_DEV void stage_touch(const DModel& m, Env& s, int lane) {
           copy3(ray, s.con_nrm[lane]);
           normalize3(ray);
           if (bid == b2) scl3(ray, ray, -1.f);
-          if (ray_geom(s.sxpos[site], s.txmat[t], &m.touch_size[3 * t], s.con_pos[lane], ray, m.touch_type[t]) >= 0.f)
+          if (ray_geom(s.sxpos[site], s.txmat[t], &m.d->touch_size[3 * t], s.con_pos[lane], ray, MD(touch_type, t)) >= 0.f)
             val = fn;
         }
       }

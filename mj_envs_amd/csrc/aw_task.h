@@ -55,7 +55,7 @@ AW_DEV float dist3(const float* a, const float* b) {
 
 // writes obs[0..obs_dim) into s.rowbuf (LDS); lane-parallel qpos copies
 AW_DEV void task_obs(const DModel& m, Env& s, int lane, float* out) {
-  const int* id = m.task_idx;
+  const int* id = m.d->task_idx;
   const int nq = m.nq, nv = m.nv;
   switch (m.task_kind) {
     case 0: {  // hammer
@@ -124,7 +124,7 @@ AW_DEV void task_obs(const DModel& m, Env& s, int lane, float* out) {
 
 // lane 0 computes reward / done / goal (fp32 restatement of the reference arithmetic)
 AW_DEV void task_reward(const DModel& m, Env& s, float* reward, int* done, int* goal) {
-  const int* id = m.task_idx;
+  const int* id = m.d->task_idx;
   float r = 0.f;
   *done = 0;
   *goal = 0;
@@ -226,7 +226,7 @@ AW_DEV void sample_params(const DModel& m, uint64_t seed, uint32_t genv, uint32_
   }
   float d[8];
 #pragma unroll
-  for (int k = 0; k < 8; k++) d[k] = k < m.ndraw ? m.draw_lo[k] + (m.draw_hi[k] - m.draw_lo[k]) * u[k] : 0.f;
+  for (int k = 0; k < 8; k++) d[k] = k < m.ndraw ? MD(draw_lo, k) + (MD(draw_hi, k) - MD(draw_lo, k)) * u[k] : 0.f;
   if (m.task_kind == 2) {
     float eu[3] = {d[0], d[1], 0.f};
     euler2quat_ref(eu, params);
