@@ -22,6 +22,23 @@ namespace aw {
 // pulls the column back with 16-byte broadcast reads for its rank-1 update.  Entries above a
 // lane's diagonal (and rows of lanes >= NV) take unmasked garbage updates that are never read:
 // the factor proper is the lower triangle of lanes < NV.
+#ifdef AW_CHOL_READLANE
+// Variant: the column is broadcast with v_readlane (SGPR operands) instead of an LDS round trip.
+template <int NV>
+AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    const float djj = fmaxf(rlane(row[j], j), MINVAL);
+    const float inv = __builtin_amdgcn_rsqf(djj);
+    const float sq = djj * inv;
+    row[j] = lane == j ? sq : row[j] * inv;
+    if (lane == j) invd = inv;
+    const float lij = row[j];
+#pragma unroll
+    for (int k = j + 1; k < NV; k++) row[k] = fmaf(-lij, rlane(lij, k), row[k]);
+  }
+}
+#else
 template <int NV>
 AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
   float* col = reinterpret_cast<float*>(s.colbuf);
@@ -50,6 +67,7 @@ AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
     }
   }
 }
+#endif
 template <int NV>
 AW_DEV void chol_store(const float (&row)[NV], int lane, Env& s) {
   if (lane < NV) {

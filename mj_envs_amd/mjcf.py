@@ -282,7 +282,7 @@ class _Compiler:
         self.bodies, self.joints, self.geoms, self.sites = [], [], [], []
         world = dict(name="world", parent=-1, pos=np.zeros(3), quat=np.array([1.0, 0, 0, 0]),
                      mass=0.0, ipos=np.zeros(3), iquat=np.array([1.0, 0, 0, 0]),
-                     inertia=np.zeros(3), mocap=False, joints=[], geoms=[], sites=[],
+                     inertia=np.zeros(3), mocap=False, joints=[], geoms=[], sites=[], cameras=[],
                      has_inertial=True, cls="main")
         self.bodies.append(world)
         wb = self.root.find("worldbody")
@@ -329,6 +329,9 @@ class _Compiler:
             elif tag == "site":
                 a = self.defaults.attrs("site", child, cls)
                 body["sites"].append(a)
+            elif tag == "camera":
+                # position only: the render camera needs cam_xpos (headless_observer.py:59-66)
+                body["cameras"].append(np.array(_floats(child.get("pos", "0 0 0"))))
             elif tag == "body":
                 children.append(child)
         for child in children:
@@ -337,7 +340,7 @@ class _Compiler:
                       pos=np.array(_floats(a.get("pos", "0 0 0"))), quat=self._orient(a),
                       mass=0.0, ipos=np.zeros(3), iquat=np.array([1.0, 0, 0, 0]),
                       inertia=np.zeros(3), mocap=a.get("mocap", "false") == "true",
-                      joints=[], geoms=[], sites=[], has_inertial=False,
+                      joints=[], geoms=[], sites=[], cameras=[], has_inertial=False,
                       cls=a.get("childclass", childclass))
             self.bodies.append(nb)
             self._read_body_contents(child, len(self.bodies) - 1, nb["cls"])
@@ -670,6 +673,9 @@ class _Compiler:
         A["site_size"] = site_size
         A["site_pos"] = site_pos
         A["site_quat"] = site_quat
+        cams = [(bi, c) for bi, b in enumerate(B) for c in b.get("cameras", [])]
+        A["cam_bodyid"] = np.array([bi for bi, _ in cams], np.int32)
+        A["cam_pos"] = np.array([c for _, c in cams], np.float64).reshape(len(cams), 3)
         A["tendon_adr"] = np.array(ten_adr, np.int32)
         A["tendon_num"] = np.array(ten_num, np.int32)
         A["tendon_limited"] = np.array(ten_limited, np.int32)
