@@ -75,6 +75,8 @@ def main():
     ap.add_argument("--envs-per-gpu", type=int, default=65536)
     ap.add_argument("--env", default=ENV_ID)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--depth", action="store_true",
+                    help="BASELINE config 5: + 64x64 depth-camera obs every env-step (default 8192 envs)")
     args = ap.parse_args()
 
     import torch
@@ -83,6 +85,8 @@ def main():
     from mj_envs_amd.dist import EpisodeGather, rank_seed, shard_from_env
     from mj_envs_amd.tasks import attach_task, load_model
 
+    if args.depth and args.envs_per_gpu == 65536:
+        args.envs_per_gpu = 8192
     shard = shard_from_env(args.envs_per_gpu)
     world, rank, local = shard.world, shard.rank, shard.local_rank
     if world > 1:
@@ -106,6 +110,11 @@ def main():
     gather = EpisodeGather(n, world, dev)
     seed = rank_seed(1, rank)                # per-rank Philox key: global env id = (rank, env)
     sim.reset(obs, seed=seed)
+    depth = cam = None
+    if args.depth:
+        from mj_envs_amd.render import free_camera
+        cam = free_camera(m, env_id, 64, 64)
+        depth = sim.empty(n, 64, 64)
 
     def one_step(k, ev=None):
         sim.random_actions(act, 1000 * rank, k)
@@ -114,6 +123,12 @@ def main():
         sim.step(act, obs, rew, done, goal, autoreset=True, seed=seed)
         if ev is not None:
             ev[1].record()
+        if depth is not None:
+            if ev is not None:
+                ev[2].record()
+            sim.render_depth(depth, cam)
+            if ev is not None:
+                ev[3].record()
         if (k + 1) % sim.horizon == 0:       # every env finished an episode this step
             sim.episode_stats(last_ret, last_goal)
             gather(last_ret, last_goal)      # RCCL all-gather over xGMI when world > 1
@@ -123,8 +138,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
+    events = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in range(args.steps)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -133,7 +147,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in events) / args.steps
+    kern_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
+    depth_ms = sum(e[2].elapsed_time(e[3]) for e in events) / args.steps if depth is not None else None
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -155,14 +170,18 @@ def main():
                     hbm_frac=round(bytes_step * n / (kern_ms * 1e-3) / 1e9 / perfmodel.PEAK_HBM_GBPS, 6),
                     note="fp32 compute roofline (VALU == f32 MFMA peak on gfx950); FLOPs from "
                          "perfmodel.py on profiles/work_counts_hammer.json")
+        workload = (f"{env_id}, {n} envs per GPU (north-star config), random policy, auto-reset at horizon "
+                    f"{sim.horizon}, RCCL all-gather of episode returns at episode ends")
+        if depth is not None:
+            workload = (f"{env_id} + 64x64 depth-camera obs (HIP ray caster, BASELINE config 5), {n} envs per "
+                        f"GPU, random policy, auto-reset at horizon {sim.horizon}")
+            roof["depth_kernel_ms"] = round(depth_ms, 4)
         line = dict(metric="env-steps/sec at N parallel envs, hammer-v0, 1/2/4/8 MI355X",
                     value=round(value, 1), unit="env-steps/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(elapsed / args.steps * 1e3, 4),
                     higher_is_better=True, scaling="weak", vs_baseline=None, dtype="f32",
                     data="synthetic (Philox U(-1,1) actions, reference reset distribution)",
-                    config=dict(workload=f"{env_id}, {n} envs per GPU (north-star config), random policy, "
-                                         f"auto-reset at horizon {sim.horizon}, RCCL all-gather of episode "
-                                         f"returns at episode ends", envs_per_gpu=n, total_envs=world * n,
+                    config=dict(workload=workload, envs_per_gpu=n, total_envs=world * n,
                                 frame_skip=sim.frame_skip, parallelism=f"env-shard x{world}"),
                     roofline=roof, finite=finite)
         if world == 1 and not args.no_cpu_baseline:

@@ -117,6 +117,18 @@ int aw_task_eval(aw_handle* h, int n, const float* qpos, const float* qvel, cons
 #define AW_DUMP_SIZE 2728
 int aw_forward_dump(aw_handle* h, int env, const float* ctrl, float* out, void* stream);
 
+/* Depth camera observation (the reference renders RGB through OpenGL:
+ * headless_observer.py:20-52 -- free camera azimuth 90, distance 4.5, elevation from the
+ * object / last-camera direction, 640x480 frame centre-cropped to 128x128 and resized to
+ * 64x64).  Ray-casts every primitive geom of every env's current state (forward kinematics
+ * of qpos) into out [N][height][width]: z-depth in metres along the camera axis, cam[AW_CAM_ZFAR]
+ * where nothing is hit.  cam: a HOST array of AW_CAM_FLOATS floats (mj_envs_amd/render.py)
+ * (position, forward, up, right, then the pixel -> image-plane map u = u0 + du*col,
+ * v = v0 - dv*row, then zfar).  Meshes (absent offline) are not rendered. */
+#define AW_CAM_FLOATS 17
+#define AW_CAM_ZFAR 16
+int aw_render_depth(aw_handle* h, const float* cam, int width, int height, float* out, void* stream);
+
 /* Diagnostic: per-stage shader-clock cycles of k_step summed over all waves since the last
  * reset (16 counters, see aw_common.h PR_*).  Only libraries built with -DAW_STAGE_PROF
  * collect them; the product build returns AW_EUNSUPPORTED. */

@@ -57,9 +57,10 @@ def load():
     L.aw_task_eval.argtypes = [_vp, ctypes.c_int] + [_vp] * 10 + [_vp]
     L.aw_forward_dump.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp]
     L.aw_stage_profile.argtypes = [_vp, ctypes.c_int]
+    L.aw_render_depth.argtypes = [_vp, _vp, ctypes.c_int, ctypes.c_int, _vp, _vp]
     for f in ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "aw_step",
               "aw_random_actions", "aw_get_state", "aw_set_state", "aw_status", "aw_episode_stats",
-              "aw_task_eval", "aw_forward_dump", "aw_stage_profile"):
+              "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_render_depth"):
         getattr(L, f).restype = ctypes.c_int
     _lib = L
     return L
@@ -67,7 +68,7 @@ def load():
 
 EXPORTS = ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "aw_step",
            "aw_random_actions", "aw_get_state", "aw_set_state", "aw_status", "aw_episode_stats",
-           "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_last_error")
+           "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_render_depth", "aw_last_error")
 
 STAGES = ("pre", "kinematics", "collision", "com_crb", "rne_smooth_solve", "constraints", "newton",
           "noslip", "jt_touch", "euler", "task_obs", "reset", "checks")
@@ -169,6 +170,15 @@ class Sim:
         _check(load().aw_task_eval(self.h, n, _ptr(qpos), _ptr(qvel), _ptr(xpos), _ptr(xquat),
                                    _ptr(site_xpos), _ptr(touch), _ptr(obs), _ptr(reward), _ptr(done),
                                    _ptr(goal), _stream()))
+
+    def render_depth(self, out, cam: np.ndarray):
+        """Depth frames of every env's current state into out [N, H, W] (device, fp32);
+        cam: the host camera record of mj_envs_amd.render.free_camera."""
+        n, h, w = out.shape
+        assert n == self.n_envs and out.is_contiguous(), "render_depth: out must be [n_envs, H, W]"
+        c = np.ascontiguousarray(cam, np.float32)
+        assert c.size == 17, "render_depth: camera record has 17 floats"
+        _check(load().aw_render_depth(self.h, c.ctypes.data, w, h, _ptr(out), _stream()))
 
     def forward_dump(self, env: int, ctrl=None) -> dict:
         import torch

@@ -17,6 +17,7 @@
 #include "aw_collide.h"
 #include "aw_common.h"
 #include "aw_dynamics.h"
+#include "aw_render.h"
 #include "aw_solver.h"
 #include "aw_task.h"
 
@@ -496,6 +497,33 @@ __global__ void __launch_bounds__(64) k_task_eval(DModel m, int n, const float* 
   }
 }
 
+// depth frame of every env's current state: wave 0 runs the kinematics, then all four waves
+// cast the pixels (one workgroup per env; render geom poses staged in LDS)
+struct CamRec {
+  float c[AW_CAM_FLOATS];
+};
+template <int NV>
+__global__ void __launch_bounds__(256) k_depth(DModel m, DState st, int n, CamRec cam, int W, int H, float* out) {
+  __shared__ Env s;
+  __shared__ RGeoms rg;
+  const int env = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  if (env >= n) return;
+  if (tid < 64) {
+    if (lane < NV) s.qpos[lane] = st.qpos[(size_t)env * m.nq + lane];
+    wsync();
+    stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
+    stage_kinematics(m, s, lane);
+  }
+  __syncthreads();
+  render_geoms(m, s, rg, tid, 256);
+  __syncthreads();
+  float* o = out + (size_t)env * W * H;
+  for (int p = tid; p < W * H; p += 256) {
+    const int row = p / W, col = p - row * W;
+    o[p] = render_pixel(rg, m.nrgeom, cam.c, row, col);
+  }
+}
+
 __global__ void k_random_actions(int n, int nu, uint64_t seed, uint64_t step, float* out) {
   int env = blockIdx.x * blockDim.x + threadIdx.x;
   if (env >= n) return;
@@ -787,6 +815,21 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
   m.ntouch = (int)ts.size();
   PUT(touch_site, ts); PUT(touch_adr, ts); PUT(touch_type, ttype); PUT(touch_size, tsize);
   {
+    // depth renderer: every primitive (non-mesh) geom in model order
+    std::vector<int> rt, rb, rc;
+    std::vector<double> rp, rq, rs, rr;
+    for (int g = 0; g < ngeom_all; g++) {
+      if (gtype[g] == 7) continue;
+      rt.push_back(gtype[g]); rb.push_back(gbody[g]); rc.push_back(gmap[g]);
+      for (int k = 0; k < 3; k++) { rp.push_back(gpos[3 * g + k]); rs.push_back(gsize[3 * g + k]); }
+      for (int k = 0; k < 4; k++) rq.push_back(gquat[4 * g + k]);
+      rr.push_back(grb[g]);
+    }
+    m.nrgeom = (int)rt.size();
+    PUT(rg_type, rt); PUT(rg_body, rb); PUT(rg_cgeom, rc); PUT(rg_pos, rp); PUT(rg_quat, rq);
+    PUT(rg_size, rs); PUT(rg_rbound, rr);
+  }
+  {
     // per-object "some parameter overrides this" flags (kinematics applies those overrides inline)
     std::vector<int> bo(nbody, 0), so(std::max(nsite, 1), 0), go(std::max(m.ngeom, 1), 0);
     for (int p = 0; p < m.nparam; p++) {
@@ -825,6 +868,11 @@ static void launch_set(aw_handle* h, const float* q, const float* v, const float
 template <int NV>
 static void launch_dump(aw_handle* h, int env, const float* ctrl, float* out, hipStream_t st) {
   hipLaunchKernelGGL((k_dump<NV>), dim3(1), dim3(64), 0, st, h->m, h->st, env, ctrl, out);
+}
+
+template <int NV>
+static void launch_depth(aw_handle* h, const CamRec& cam, int W, int H, float* out, hipStream_t st) {
+  hipLaunchKernelGGL((k_depth<NV>), dim3(h->nenv), dim3(256), 0, st, h->m, h->st, h->nenv, cam, W, H, out);
 }
 
 #ifdef AW_ONLY_NV
@@ -1010,6 +1058,19 @@ int aw_forward_dump(aw_handle* h, int env, const float* ctrl, float* out, void* 
   if (!h || !out || env < 0 || env >= h->nenv) return fail(AW_EINVAL, "aw_forward_dump: bad arguments");
   HIPCHK(hipSetDevice(h->device));
 #define CALL(NVV) launch_dump<NVV>(h, env, ctrl, out, (hipStream_t)stream)
+  DISPATCH_NV(h->NV, CALL)
+#undef CALL
+  HIPCHK(hipGetLastError());
+  return AW_OK;
+}
+
+int aw_render_depth(aw_handle* h, const float* cam, int width, int height, float* out, void* stream) {
+  if (!h || !cam || !out || width <= 0 || height <= 0 || width > 4096 || height > 4096)
+    return fail(AW_EINVAL, "aw_render_depth: bad arguments");
+  HIPCHK(hipSetDevice(h->device));
+  CamRec c;
+  memcpy(c.c, cam, sizeof(c.c));   // host array: the camera record travels as a kernel argument
+#define CALL(NVV) launch_depth<NVV>(h, c, width, height, out, (hipStream_t)stream)
   DISPATCH_NV(h->NV, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());

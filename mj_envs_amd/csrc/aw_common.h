@@ -89,6 +89,7 @@ enum { ST_BADQPOS = 1, ST_BADQVEL = 2, ST_BADQACC = 4, ST_CON_OVERFLOW = 8, ST_E
 // compiler keep ~100 per-lane 64-bit addresses live across a substep -- spills.)
 constexpr int MAXPAIR = 320;  // explicit pairs + broadphase candidates
 constexpr int MAXTIDX = 16;   // task object ids
+constexpr int MAXRG = 64;     // rendered (primitive) geoms
 
 #define AW_MODEL_ARRAYS(X)                                                                     \
   X(int, body_parentid, MAXB) X(int, body_rootid, MAXB) X(int, body_dofnum, MAXB)               \
@@ -126,7 +127,11 @@ constexpr int MAXTIDX = 16;   // task object ids
   X(int, body_ovr, MAXB) X(int, site_ovr, MAXS) X(int, geom_ovr, MAXG) /* 1: overridden */    \
   X(int, task_idx, MAXTIDX) X(int, param_field, MAXP) X(int, param_obj, MAXP)                   \
   X(int, param_comp, MAXP) X(float, act_mid, MAXU) X(float, act_rng, MAXU)                      \
-  X(float, param_default, MAXP) X(float, draw_lo, 8) X(float, draw_hi, 8)
+  X(float, param_default, MAXP) X(float, draw_lo, 8) X(float, draw_hi, 8)                      \
+  /* depth renderer: every primitive geom (model order), its collidable index or -1 */        \
+  X(int, rg_type, MAXRG) X(int, rg_body, MAXRG) X(int, rg_cgeom, MAXRG)                         \
+  X(float, rg_pos, MAXRG * 3) X(float, rg_quat, MAXRG * 4) X(float, rg_size, MAXRG * 3)         \
+  X(float, rg_rbound, MAXRG)
 
 struct MData {
 #define AW_X(T, name, n) T name[n];
@@ -152,6 +157,7 @@ struct DModel {
   float timestep, gravity[3], tolerance, noslip_tolerance, mpr_tolerance, meaninertia;
   float pen_length, tar_length;
   int cls_start[NCLASS + 1];  // collider class c owns pair-list slots [cls_start[c], cls_start[c+1])
+  int nrgeom;                 // rendered geoms
   const MData* __restrict__ d;
 };
 
