@@ -75,6 +75,8 @@ def main():
     ap.add_argument("--envs-per-gpu", type=int, default=65536)
     ap.add_argument("--env", default=ENV_ID)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--policy", action="store_true",
+                    help="closed loop: actions from the on-device Gaussian MLP (mjrl MLP, 32x32) instead of i.i.d.")
     ap.add_argument("--depth", action="store_true",
                     help="BASELINE config 5: + 64x64 depth-camera obs every env-step (default 8192 envs)")
     args = ap.parse_args()
@@ -110,6 +112,10 @@ def main():
     gather = EpisodeGather(n, world, dev)
     seed = rank_seed(1, rank)                # per-rank Philox key: global env id = (rank, env)
     sim.reset(obs, seed=seed)
+    pol = None
+    if args.policy:
+        from mj_envs_amd.policy import GaussianMLP
+        pol = GaussianMLP(sim.obs_dim, sim.nu, (32, 32), init_log_std=-1.0, seed=0, device=local)
     depth = cam = None
     if args.depth:
         from mj_envs_amd.render import free_camera
@@ -117,7 +123,10 @@ def main():
         depth = sim.empty(n, 64, 64)
 
     def one_step(k, ev=None):
-        sim.random_actions(act, 1000 * rank, k)
+        if pol is not None:
+            pol.act(obs, out=act, sample=True, seed=1000 * rank, step=k)
+        else:
+            sim.random_actions(act, 1000 * rank, k)
         if ev is not None:
             ev[0].record()
         sim.step(act, obs, rew, done, goal, autoreset=True, seed=seed)
@@ -172,6 +181,9 @@ def main():
                          "perfmodel.py on profiles/work_counts_hammer.json")
         workload = (f"{env_id}, {n} envs per GPU (north-star config), random policy, auto-reset at horizon "
                     f"{sim.horizon}, RCCL all-gather of episode returns at episode ends")
+        if pol is not None:
+            workload = workload.replace("random policy", "closed loop with the on-device Gaussian MLP policy "
+                                        "(mjrl MLP 32x32, random init, sampled actions)")
         if depth is not None:
             workload = (f"{env_id} + 64x64 depth-camera obs (HIP ray caster, BASELINE config 5), {n} envs per "
                         f"GPU, random policy, auto-reset at horizon {sim.horizon}")

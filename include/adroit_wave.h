@@ -129,6 +129,16 @@ int aw_forward_dump(aw_handle* h, int env, const float* ctrl, float* out, void* 
 #define AW_CAM_ZFAR 16
 int aw_render_depth(aw_handle* h, const float* cam, int width, int height, float* out, void* stream);
 
+/* On-device Gaussian MLP policy: mjrl gaussian_mlp.MLP as used by the
+ * reference's DAPG baseline (algos/baselines.py:67-86, hidden_sizes=(32, 32)) -- two tanh
+ * hidden layers of width `hidden` (32 or 64), in/out affine transforms, and with sample != 0
+ * the Gaussian exploration noise exp(log_std) * N(0, 1) (Philox, key = seed, counter =
+ * (env, step)); sample == 0 returns the mean (get_action(...)[1]['evaluation']).
+ * params: device fp32 block, layout in mj_envs_amd/csrc/aw_policy.h; obs [n][in_dim] ->
+ * act [n][out_dim], in_dim <= 64, out_dim <= 32.  Stateless: no handle. */
+int aw_policy_mlp(int n, int in_dim, int hidden, int out_dim, const float* params, const float* obs,
+                  float* act, int sample, uint64_t seed, uint64_t step, void* stream);
+
 /* Diagnostic: per-stage shader-clock cycles of k_step summed over all waves since the last
  * reset (16 counters, see aw_common.h PR_*).  Only libraries built with -DAW_STAGE_PROF
  * collect them; the product build returns AW_EUNSUPPORTED. */

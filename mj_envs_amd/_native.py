@@ -58,9 +58,10 @@ def load():
     L.aw_forward_dump.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp]
     L.aw_stage_profile.argtypes = [_vp, ctypes.c_int]
     L.aw_render_depth.argtypes = [_vp, _vp, ctypes.c_int, ctypes.c_int, _vp, _vp]
+    L.aw_policy_mlp.argtypes = [ctypes.c_int] * 4 + [_vp, _vp, _vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, _vp]
     for f in ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "aw_step",
               "aw_random_actions", "aw_get_state", "aw_set_state", "aw_status", "aw_episode_stats",
-              "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_render_depth"):
+              "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_render_depth", "aw_policy_mlp"):
         getattr(L, f).restype = ctypes.c_int
     _lib = L
     return L
@@ -68,7 +69,7 @@ def load():
 
 EXPORTS = ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "aw_step",
            "aw_random_actions", "aw_get_state", "aw_set_state", "aw_status", "aw_episode_stats",
-           "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_render_depth", "aw_last_error")
+           "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_render_depth", "aw_policy_mlp", "aw_last_error")
 
 STAGES = ("pre", "kinematics", "collision", "com_crb", "rne_smooth_solve", "constraints", "newton",
           "noslip", "jt_touch", "euler", "task_obs", "reset", "checks")

@@ -18,6 +18,7 @@
 #include "aw_common.h"
 #include "aw_dynamics.h"
 #include "aw_render.h"
+#include "aw_policy.h"
 #include "aw_solver.h"
 #include "aw_task.h"
 
@@ -1073,6 +1074,21 @@ int aw_render_depth(aw_handle* h, const float* cam, int width, int height, float
 #define CALL(NVV) launch_depth<NVV>(h, c, width, height, out, (hipStream_t)stream)
   DISPATCH_NV(h->NV, CALL)
 #undef CALL
+  HIPCHK(hipGetLastError());
+  return AW_OK;
+}
+
+int aw_policy_mlp(int n, int in_dim, int hidden, int out_dim, const float* params, const float* obs, float* act,
+                  int sample, uint64_t seed, uint64_t step, void* stream) {
+  if (n <= 0 || !params || !obs || !act || in_dim <= 0 || in_dim > MLP_IMAX || out_dim <= 0 || out_dim > MLP_OMAX)
+    return fail(AW_EINVAL, "aw_policy_mlp: bad arguments");
+  const int bs = 256, nb = (n + bs - 1) / bs;
+  hipStream_t st = (hipStream_t)stream;
+  switch (hidden) {
+    case 32: hipLaunchKernelGGL(k_mlp<32>, dim3(nb), dim3(bs), 0, st, n, in_dim, out_dim, params, obs, act, sample, seed, step); break;
+    case 64: hipLaunchKernelGGL(k_mlp<64>, dim3(nb), dim3(bs), 0, st, n, in_dim, out_dim, params, obs, act, sample, seed, step); break;
+    default: return fail(AW_EUNSUPPORTED, "aw_policy_mlp: hidden width must be 32 or 64 (two hidden layers)");
+  }
   HIPCHK(hipGetLastError());
   return AW_OK;
 }

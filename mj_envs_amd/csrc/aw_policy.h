@@ -1,0 +1,89 @@
+// aw_policy.h -- on-device Gaussian MLP policy.
+//
+// Restates mjrl's gaussian_mlp.MLP / FCNetwork (third-party, unpinned git master; used by the
+// reference's DAPG baseline, mj_envs_vision/algos/baselines.py:67-86 with hidden_sizes=(32, 32)):
+//   out = (obs - in_shift) / (in_scale + 1e-8); out = tanh(W0 out + b0); out = tanh(W1 out + b1);
+//   mean = (W2 out + b2) * out_scale + out_shift;  action = mean [+ exp(log_std) * N(0, 1)].
+// One thread per env; the parameters are read with uniform addresses (scalar loads), the
+// activations stay in VGPRs.  Parameter block layout (fp32):
+//   in_shift[in] in_scale[in] W0[H][in] b0[H] W1[H][H] b1[H] W2[out][H] b2[out]
+//   out_scale[out] out_shift[out] log_std[out]
+#pragma once
+#include "aw_common.h"
+#include "aw_task.h"
+
+namespace aw {
+
+constexpr int MLP_IMAX = 64;   // observation width cap
+constexpr int MLP_OMAX = 32;   // action width cap
+
+AW_DEV int mlp_param_count(int in, int h, int out) { return 2 * in + h * in + h + h * h + h + out * h + 4 * out; }
+
+template <int H>
+__global__ void __launch_bounds__(256) k_mlp(int n, int in, int out, const float* __restrict__ p,
+                                             const float* __restrict__ obs, float* __restrict__ act, int sample,
+                                             uint64_t seed, uint64_t step) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const float* in_shift = p;
+  const float* in_scale = p + in;
+  const float* W0 = p + 2 * in;
+  const float* b0 = W0 + H * in;
+  const float* W1 = b0 + H;
+  const float* b1 = W1 + H * H;
+  const float* W2 = b1 + H;
+  const float* b2 = W2 + out * H;
+  const float* osc = b2 + out;
+  const float* osh = osc + out;
+  const float* lstd = osh + out;
+  float x[MLP_IMAX];
+#pragma unroll
+  for (int k = 0; k < MLP_IMAX; k++)
+    x[k] = k < in ? (obs[(size_t)e * in + k] - in_shift[k]) / (in_scale[k] + 1e-8f) : 0.f;
+  float h1[H], h2[H];
+#pragma unroll
+  for (int j = 0; j < H; j++) {
+    float acc = b0[j];
+#pragma unroll
+    for (int k = 0; k < MLP_IMAX; k++)
+      if (k < in) acc = fmaf(W0[j * in + k], x[k], acc);
+    h1[j] = tanhf(acc);
+  }
+#pragma unroll
+  for (int j = 0; j < H; j++) {
+    float acc = b1[j];
+#pragma unroll
+    for (int k = 0; k < H; k++) acc = fmaf(W1[j * H + k], h1[k], acc);
+    h2[j] = tanhf(acc);
+  }
+  float nz[MLP_OMAX];
+#pragma unroll
+  for (int o = 0; o < MLP_OMAX; o++) nz[o] = 0.f;
+  if (sample) {
+    // N(0, 1) by Box-Muller on Philox draws, counter = (env, step, 0x901C, block)
+#pragma unroll
+    for (int blk = 0; blk < MLP_OMAX / 4; blk++) {
+      uint32_t c[4] = {(uint32_t)e, (uint32_t)step, (uint32_t)(step >> 32) ^ 0x901Cu, (uint32_t)blk};
+      philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const float u1 = fmaxf(u01(c[2 * q]), 1.0f / 16777216.0f), u2 = u01(c[2 * q + 1]);
+        const float r = sqrtf(-2.f * logf(u1));
+        nz[4 * blk + 2 * q] = r * cosf(6.28318530717958647f * u2);
+        nz[4 * blk + 2 * q + 1] = r * sinf(6.28318530717958647f * u2);
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < MLP_OMAX; o++) {
+    if (o >= out) break;
+    float acc = b2[o];
+#pragma unroll
+    for (int k = 0; k < H; k++) acc = fmaf(W2[o * H + k], h2[k], acc);
+    float a = acc * osc[o] + osh[o];
+    if (sample) a = fmaf(expf(lstd[o]), nz[o], a);
+    act[(size_t)e * out + o] = a;
+  }
+}
+
+}  // namespace aw
