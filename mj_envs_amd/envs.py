@@ -103,6 +103,18 @@ class AdroitVecEnv:
         self.sim.random_actions(out, seed, step)
         return out
 
+    def render_depth(self, width: int = 64, height: int = 64, out=None):
+        """Depth frames [N, height, width] (metres, device) of every env's current state from
+        the reference's headless camera (headless_observer.py; mj_envs_amd/render.py)."""
+        from .render import free_camera
+        key = (width, height)
+        if getattr(self, "_cam_key", None) != key:
+            self._cam, self._cam_key = free_camera(self.model, self.env_id, width, height), key
+        if out is None:
+            out = self.sim.empty(self.num_envs, height, width)
+        self.sim.render_depth(out, self._cam)
+        return out
+
     # --- state -----------------------------------------------------------------------------
     def get_state(self) -> Dict[str, "object"]:
         s = self.sim
@@ -211,7 +223,10 @@ class _AdroitEnv:
         return _evaluate_success(self.env_id, paths)
 
     def render(self, *args, **kwargs):
-        raise NotImplementedError("rendering is outside the accelerated path (see DESIGN.md, out of scope)")
+        """Depth frame [height, width] (float64, metres) of the current state.  The reference
+        returns an RGB frame from OpenGL (headless_observer.py:34-52); RGB is not rendered here,
+        the HIP ray caster produces metric depth from the same camera (mj_envs_amd/render.py)."""
+        return self.vec.render_depth(self.width, self.height)[0].cpu().numpy().astype(np.float64)
 
     def close(self):
         self.vec.close()
