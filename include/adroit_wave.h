@@ -140,7 +140,7 @@ int aw_policy_mlp(int n, int in_dim, int hidden, int out_dim, const float* param
                   float* act, int sample, uint64_t seed, uint64_t step, void* stream);
 
 /* Diagnostic: per-stage shader-clock cycles of k_step summed over all waves since the last
- * reset (16 counters, see aw_common.h PR_*).  Only libraries built with -DAW_STAGE_PROF
+ * reset (40 counters, see aw_common.h PR_*).  Only libraries built with -DAW_STAGE_PROF
  * collect them; the product build returns AW_EUNSUPPORTED. */
 int aw_stage_profile(unsigned long long* out, int reset);
 

@@ -73,12 +73,13 @@ EXPORTS = ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "a
 
 STAGES = ("pre", "kinematics", "collision", "com_crb", "rne_smooth_solve", "constraints", "newton",
           "noslip", "jt_touch", "euler", "task_obs", "reset", "checks")
-SUBSTAGES = ("nt_init", "nt_hess", "nt_chol", "nt_solve", "nt_ls", "nt_upd", "ns_minv", "ns_setup", "ns_iter")
+SUBSTAGES = ("nt_init", "nt_hess", "nt_chol", "nt_solve", "nt_ls", "nt_upd", "ns_minv", "ns_setup", "ns_iter",
+             "co_broad", "co_narrow", "com", "rne", "co_plane", "co_round", "co_roundbox", "co_boxbox")
 
 
 def stage_profile(reset: bool = True) -> dict:
     """Per-stage shader-clock cycles of k_step (diagnostic build only, see aw_stage_profile)."""
-    buf = (ctypes.c_ulonglong * 32)()
+    buf = (ctypes.c_ulonglong * 40)()
     _check(load().aw_stage_profile(buf, int(reset)))
     v = list(buf)
     out = {name: v[i] for i, name in enumerate(STAGES)}

@@ -71,6 +71,13 @@ AW_DEV void sort_contacts(Env& s, int lane) {
   wsync();
 }
 
+// narrowphase over the broadphase survivors of one collider class
+template <int C>
+AW_DEV void narrow_class(const DModel& m, Env& s, const short* plist, int cnt, int lane) {
+  const int st = m.cls_start[C];
+  for (int i = lane; i < cnt; i += 64) collide_pair<C>(m, s, plist[st + i]);
+}
+
 // mj_collision: bounding-sphere broadphase over the static candidate list (one pair per lane,
 // 64 per round), survivors compacted class-major into an LDS list (ballot + mbcnt), then ONE
 // narrowphase loop over the list: lanes of a round mostly share a collider, instead of every
@@ -108,23 +115,20 @@ AW_DEV void stage_collision(const DModel& m, Env& s, int lane) {
         cnt[c] += __popcll(mask);
       }
     }
-    int pre[NCLASS + 1];
-    pre[0] = 0;
-#pragma unroll
-    for (int c = 0; c < NCLASS; c++) pre[c + 1] = pre[c] + cnt[c];
+    AW_PROF(s, PR_CO_BROAD);
     wsync();
-    for (int i = lane; i < pre[NCLASS]; i += 64) {
-      int c = 0;
-#pragma unroll
-      for (int k = 1; k < NCLASS; k++) c += i >= pre[k] ? 1 : 0;
-      int off = i, st = 0;
-#pragma unroll
-      for (int k = 0; k < NCLASS; k++)
-        if (k == c) { off = i - pre[k]; st = m.cls_start[k]; }
-      collide_pair(m, s, plist[st + off]);
-    }
+    narrow_class<0>(m, s, plist, cnt[0], lane);
+    AW_PROF(s, PR_CO_C0);
+    narrow_class<1>(m, s, plist, cnt[1], lane);
+    AW_PROF(s, PR_CO_C1);
+    narrow_class<2>(m, s, plist, cnt[2], lane);
+    AW_PROF(s, PR_CO_C2);
+    narrow_class<3>(m, s, plist, cnt[3], lane);
+    AW_PROF(s, PR_CO_C3);
+    narrow_class<4>(m, s, plist, cnt[4], lane);
   }
   wsync();
+  AW_PROF(s, PR_CO_NARROW);
   sort_contacts(s, lane);
 }
 
@@ -143,8 +147,9 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV], Dof& d
   stage_collision(m, s, lane);
   AW_PROF(s, PR_COLL);
   stage_com(m, s, lane);
+  AW_PROF(s, PR_COM);
   d.qfrc_smooth = stage_velocity(m, s, lane);
-  AW_PROF(s, PR_SMOOTH);
+  AW_PROF(s, PR_RNE);
   stage_crb<NV>(m, s, lane, Mrow);
   AW_PROF(s, PR_CRB);
   if (lane == 0) { s.it_newton = 0; s.it_noslip = 0; }

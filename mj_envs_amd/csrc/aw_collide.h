@@ -214,43 +214,44 @@ AW_DEV void c_sphere_box_pt(const float* p, float r, const GV& b, float margin, 
   emit(e, dist, pos, n);
 }
 
-AW_DEV float box_sdist(const float* p, const GV& b) {
-  float dif[3], loc[3];
-  sub3(dif, p, b.pos);
-  mulmtv3(loc, b.mat, dif);
-  float out = 0, mx = -1e30f;
-  for (int k = 0; k < 3; k++) {
-    float q = fabsf(loc[k]) - b.size[k];
-    float qp = q > 0 ? q : 0;
-    out += qp * qp;
-    mx = fmaxf(mx, q);
-  }
-  return sqrtf(out) + (mx < 0 ? mx : 0);
-}
-
 AW_DEV void c_capsule_box(const GV& a, const GV& b, float margin, Emit& e) {
   float ax[3], p[3];
   axis_of(ax, a.mat, 2);
-  float h = a.size[1], r = a.size[0];
+  const float h = a.size[1], r = a.size[0];
+  // the capsule axis in the box frame: q(t) = c + t u, so each signed-distance evaluation of
+  // the golden-section search is 3 FMAs + the box distance (no per-point rotation)
+  float dif[3], c[3], u[3];
+  sub3(dif, a.pos, b.pos);
+  mulmtv3(c, b.mat, dif);
+  mulmtv3(u, b.mat, ax);
+  auto sd = [&](float t) {
+    float out = 0.f, mx = -1e30f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const float q = fabsf(fmaf(t, u[k], c[k])) - b.size[k];
+      const float qp = fmaxf(q, 0.f);
+      out = fmaf(qp, qp, out);
+      mx = fmaxf(mx, q);
+    }
+    return sqrtf(out) + fminf(mx, 0.f);
+  };
   const float gr = 0.6180339887498949f;
   float lo = -h, hi = h;
   float x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo);
-  for (int k = 0; k < 3; k++) p[k] = a.pos[k] + ax[k] * x1;
-  float f1 = box_sdist(p, b);
-  for (int k = 0; k < 3; k++) p[k] = a.pos[k] + ax[k] * x2;
-  float f2 = box_sdist(p, b);
+  float f1 = sd(x1), f2 = sd(x2);
+  // branch-free (lanes hold different pairs): select the shrunk bracket, evaluate one point
   for (int it = 0; it < 40; it++) {
-    if (f1 < f2) {
-      hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
-      for (int k = 0; k < 3; k++) p[k] = a.pos[k] + ax[k] * x1;
-      f1 = box_sdist(p, b);
-    } else {
-      lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
-      for (int k = 0; k < 3; k++) p[k] = a.pos[k] + ax[k] * x2;
-      f2 = box_sdist(p, b);
-    }
+    const bool l = f1 < f2;
+    const float nhi = l ? x2 : hi, nlo = l ? lo : x1;
+    const float nx1 = l ? nhi - gr * (nhi - nlo) : x2;
+    const float nx2 = l ? x1 : nlo + gr * (nhi - nlo);
+    const float fe = sd(l ? nx1 : nx2);
+    const float of1 = f1, of2 = f2;
+    f1 = l ? fe : of2;
+    f2 = l ? of1 : fe;
+    hi = nhi; lo = nlo; x1 = nx1; x2 = nx2;
   }
-  float ts = 0.5f * (lo + hi);
+  const float ts = 0.5f * (lo + hi);
   for (int k = 0; k < 3; k++) p[k] = a.pos[k] + ax[k] * ts;
   int before = e.cnt;
   c_sphere_box_pt(p, r, b, margin, e);
@@ -707,6 +708,11 @@ AW_DEV void c_convex(const DModel& m, const GV& a, const GV& b, float margin, Em
 }
 
 // ---------------------------------------------------------------------------------------
+// narrowphase of one pair of collider class C (host: adroit_wave.hip build_model pcls):
+// 0 plane-*, 1 sphere/capsule pairs, 2 sphere/capsule-box, 3 box-box, 4 anything with a
+// cylinder (MPR).  The class is a template parameter so each class loop carries only its own
+// colliders (no divergent merge of every collider's code and registers).
+template <int C>
 AW_DEV void collide_pair(const DModel& m, Env& s, int pair) {
   int g1 = MD(cp_g1, pair), g2 = MD(cp_g2, pair);
   GV a, b;
@@ -724,30 +730,22 @@ AW_DEV void collide_pair(const DModel& m, Env& s, int pair) {
     q2m(b.mat, q2);
   }
   Emit e{&s, pair, 0};
-  // every non-plane pair with a cylinder goes through MPR (mjc_Convex); one inlined call site
-  if (a.type != GEOM_PLANE && (a.type == GEOM_CYLINDER || b.type == GEOM_CYLINDER)) {
+  if constexpr (C == 4) {           // every non-plane pair with a cylinder: MPR (mjc_Convex)
     c_convex(m, a, b, margin, e);
-    return;
-  }
-  switch (a.type) {
-    case GEOM_PLANE:
-      if (b.type == GEOM_SPHERE) c_plane_sphere(a.pos, a.mat, b.pos, b.size[0], margin, e);
-      else if (b.type == GEOM_CAPSULE) c_plane_capsule(a, b, margin, e);
-      else if (b.type == GEOM_CYLINDER) c_plane_cylinder(a, b, margin, e);
-      else if (b.type == GEOM_BOX) c_plane_box(a, b, margin, e);
-      break;
-    case GEOM_SPHERE:
-      if (b.type == GEOM_SPHERE) c_sphere_sphere(a.pos, a.size[0], b.pos, b.size[0], margin, e);
-      else if (b.type == GEOM_CAPSULE) c_sphere_capsule(a, b, margin, e);
-      else if (b.type == GEOM_BOX) c_sphere_box_pt(a.pos, a.size[0], b, margin, e);
-      break;
-    case GEOM_CAPSULE:
-      if (b.type == GEOM_CAPSULE) c_capsule_capsule(a, b, margin, e);
-      else if (b.type == GEOM_BOX) c_capsule_box(a, b, margin, e);
-      break;
-    case GEOM_BOX:
-      if (b.type == GEOM_BOX) c_box_box(a, b, margin, e);
-      break;
+  } else if constexpr (C == 0) {
+    if (b.type == GEOM_SPHERE) c_plane_sphere(a.pos, a.mat, b.pos, b.size[0], margin, e);
+    else if (b.type == GEOM_CAPSULE) c_plane_capsule(a, b, margin, e);
+    else if (b.type == GEOM_CYLINDER) c_plane_cylinder(a, b, margin, e);
+    else if (b.type == GEOM_BOX) c_plane_box(a, b, margin, e);
+  } else if constexpr (C == 1) {
+    if (a.type == GEOM_SPHERE && b.type == GEOM_SPHERE) c_sphere_sphere(a.pos, a.size[0], b.pos, b.size[0], margin, e);
+    else if (a.type == GEOM_SPHERE) c_sphere_capsule(a, b, margin, e);
+    else c_capsule_capsule(a, b, margin, e);
+  } else if constexpr (C == 2) {
+    if (a.type == GEOM_SPHERE) c_sphere_box_pt(a.pos, a.size[0], b, margin, e);
+    else c_capsule_box(a, b, margin, e);
+  } else {
+    c_box_box(a, b, margin, e);
   }
 }
 
