@@ -57,11 +57,18 @@ def load():
     L.aw_task_eval.argtypes = [_vp, ctypes.c_int] + [_vp] * 10 + [_vp]
     L.aw_forward_dump.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp]
     L.aw_stage_profile.argtypes = [_vp, ctypes.c_int]
-    L.aw_render_depth.argtypes = [_vp, _vp, ctypes.c_int, ctypes.c_int, _vp, _vp]
-    L.aw_policy_mlp.argtypes = [ctypes.c_int] * 4 + [_vp, _vp, _vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, _vp]
+    # (diagnostic builds of older revisions, selected with AW_LIB, may lack the newer entry points;
+    # calling one of those then raises AttributeError)
+    if hasattr(L, "aw_render_depth"):
+        L.aw_render_depth.argtypes = [_vp, _vp, ctypes.c_int, ctypes.c_int, _vp, _vp]
+        L.aw_render_depth.restype = ctypes.c_int
+    if hasattr(L, "aw_policy_mlp"):
+        L.aw_policy_mlp.argtypes = [ctypes.c_int] * 4 + [_vp, _vp, _vp, ctypes.c_int, ctypes.c_uint64,
+                                                         ctypes.c_uint64, _vp]
+        L.aw_policy_mlp.restype = ctypes.c_int
     for f in ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "aw_step",
               "aw_random_actions", "aw_get_state", "aw_set_state", "aw_status", "aw_episode_stats",
-              "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_render_depth", "aw_policy_mlp"):
+              "aw_task_eval", "aw_forward_dump", "aw_stage_profile"):
         getattr(L, f).restype = ctypes.c_int
     _lib = L
     return L

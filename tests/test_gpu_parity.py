@@ -236,3 +236,56 @@ def test_determinism():
         torch.cuda.synchronize()
         outs.append(obs.clone())
     assert torch.equal(outs[0], outs[1])
+
+
+# Minimum fraction of (env, step) cases within the one-step tolerance.  pen-v0 is lower: while
+# the pen falls onto the fingers |qacc| reaches ~1e3, the fp32 Newton solution carries ~1e-3
+# absolute error into the residuals of the (unconverged, tolerance 1e-6) noslip PGS, whose early
+# exit then lands one sweep apart from the fp64 oracle's (6 vs 5 sweeps: ~1 % qacc change in that
+# substep).  tools/debug_sub.py shows forward internals identical to 4e-7 relative up to that
+# substep.
+TEACHER_FORCED_MIN = {"hammer-v0": 0.95, "door-v0": 0.95, "relocate-v0": 0.95, "pen-v0": 0.75}
+
+
+@pytest.mark.parametrize("env_id", ENVS)
+def test_teacher_forced_trajectory(env_id):
+    """SURVEY §8d C3 (multi-task correctness vs the CPU path): along a 40-step GPU rollout of
+    64 envs, every env-step is re-run by the fp64 oracle from the GPU's own pre-step state
+    (qpos, qvel, warmstart, params) with the same action; the GPU's post-step state must match
+    within the one-step tolerance in the 2 560 (env, step) cases.  Teacher forcing
+    keeps the comparison per-step: free-running fp32 vs fp64 contact trajectories diverge
+    (chaos), which says nothing about either.  Thresholds: TEACHER_FORCED_MIN."""
+    from mj_envs_amd.tasks import sample_params
+    n, steps = 64, 40
+    m, o = make_oracle(env_id)
+    o.set_option(max_con=32, max_efc=128)
+    _, sim = _sim(env_id, n)
+    P = sample_params(env_id, m, np.random.default_rng(11), n)
+    obs = sim.empty(n, sim.obs_dim)
+    sim.reset(obs, params=_t(P))
+    rew = sim.empty(n)
+    done, goal = sim.empty(n, dtype=torch.uint8), sim.empty(n, dtype=torch.uint8)
+    q, v, w = sim.empty(n, sim.nq), sim.empty(n, sim.nv), sim.empty(n, sim.nv)
+    rng = np.random.default_rng(13)
+    oks, rok = [], []
+    for k in range(steps):
+        sim.get_state(q, v, w)
+        torch.cuda.synchronize()
+        st = dict(qpos=q.cpu().numpy().astype(np.float64), qvel=v.cpu().numpy().astype(np.float64),
+                  warm=w.cpu().numpy().astype(np.float64), params=np.asarray(P, np.float64))
+        act = rng.uniform(-1, 1, (n, sim.nu))
+        sim.step(_t(act), obs, rew, done, goal)
+        sim.get_state(q, v)
+        torch.cuda.synchronize()
+        _, r_ref, _, _, _ = o.step(st, act, nthreads=8)
+        qg, vg = q.cpu().numpy(), v.cpu().numpy()
+        okq = (np.abs(qg - st["qpos"]) <= 2e-5 + 1e-5 * np.abs(st["qpos"])).all(axis=1)
+        okv = (np.abs(vg - st["qvel"]) <= 5e-3 * (1 + np.abs(st["qvel"]))).all(axis=1)
+        ok = okq & okv
+        oks.append(ok)
+        rg = rew.cpu().numpy()
+        rok.append(np.abs(rg - r_ref)[ok] <= 1e-3 + 1e-3 * np.abs(r_ref[ok]))
+    frac = np.concatenate(oks).mean()
+    print(f"teacher-forced {env_id}: {frac:.4f} of (env, step) cases within tolerance")
+    assert frac >= TEACHER_FORCED_MIN[env_id], (env_id, frac)
+    assert np.concatenate(rok).all(), env_id
