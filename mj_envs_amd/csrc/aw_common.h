@@ -15,7 +15,7 @@
 namespace aw {
 
 constexpr int MAXV = 36;      // dofs (relocate: 36)
-constexpr int VS = 37;        // odd row stride for [.][MAXV] LDS matrices (bank-conflict free)
+constexpr int VS = 36;        // J row stride: 144 B rows keep 16-byte alignment, so broadcast reads of a row are ds_read_b128
 constexpr int MAXB = 32;      // bodies incl. world
 constexpr int MAXG = 36;      // collidable geoms (compact list)
 constexpr int MAXS = 32;      // sites
@@ -173,8 +173,10 @@ struct DModel {
 //   phase K      kinematics / com / RNE / CRB temporaries, dead once the Jacobian exists
 //   phase S      packed Cholesky factor and solver vectors (smooth solve, Newton, noslip, Euler)
 // dof vectors with only lane-local use (qacc, qacc_smooth, qfrc_smooth, qfrc_con) are VGPRs.
-constexpr int NPACK = MAXV * (MAXV + 1) / 2;   // packed lower triangle, row j at j(j+1)/2
-AW_DEV constexpr int tri(int j) { return j * (j + 1) / 2; }
+// packed lower triangle with every row padded to a multiple of 4 floats: row j starts at a
+// 16-byte aligned tri(j), so uniform reads along a row are ds_read_b128 broadcasts
+__host__ __device__ constexpr int tri(int j) { return 4 * (j + 2 * (j / 4) * (j / 4 - 1) + (j % 4) * (j / 4)); }
+constexpr int NPACK = tri(MAXV);
 
 struct __attribute__((aligned(16))) Env {
   union {
@@ -190,7 +192,7 @@ struct __attribute__((aligned(16))) Env {
     };
     struct {  // phase S
       float4 colbuf[16];      // Cholesky column broadcast (64 floats, 16-byte aligned for b128 reads)
-      float L[NPACK];         // Cholesky factor, packed lower triangle
+      float L[NPACK];         // Cholesky factor, packed lower triangle (rows padded to 4)
       float vec[MAXV], vec2[MAXV], hdiag[MAXV];
     };
   };
@@ -213,7 +215,7 @@ struct __attribute__((aligned(16))) Env {
   signed char efc_i0[MAXEFC], efc_i1[MAXEFC];
   float efc_v0[MAXEFC], efc_v1[MAXEFC], efc_floss[MAXEFC], efc_D[MAXEFC];
   float efc_aref[MAXEFC], efc_force[MAXEFC];
-  float J[MAXDENSE][VS];
+  float J[MAXDENSE][VS] __attribute__((aligned(16)));
   float rowbuf[MAXEFC];
   unsigned status;
   int it_newton, it_noslip;   // iterations of the last solve (introspection)
