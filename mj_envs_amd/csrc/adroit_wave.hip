@@ -652,7 +652,7 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
     for (int a = dparent[j]; a >= 0; a = dparent[a]) amask[j] |= 1ull << a;
 
   PUT(body_parentid, parent); PUT(body_rootid, rootid); PUT(body_dofnum, dofnum);
-  PUT(body_dofadr, dofadr); PUT(body_subtree_end, send); PUT(level_start, lstart);
+  PUT(body_dofadr, dofadr); PUT(body_depth, depth); PUT(body_subtree_end, send); PUT(level_start, lstart);
   PUT(level_body, lbody);
   PUT(body_pos, tof(B.f("body_pos"))); PUT(body_quat, tof(B.f("body_quat")));
   PUT(body_ipos, tof(B.f("body_ipos"))); PUT(body_iquat, tof(B.f("body_iquat")));

@@ -94,7 +94,7 @@ constexpr int MAXRG = 64;     // rendered (primitive) geoms
 
 #define AW_MODEL_ARRAYS(X)                                                                     \
   X(int, body_parentid, MAXB) X(int, body_rootid, MAXB) X(int, body_dofnum, MAXB)               \
-  X(int, body_dofadr, MAXB) X(int, body_subtree_end, MAXB) X(int, level_start, MAXLEV + 1)      \
+  X(int, body_dofadr, MAXB) X(int, body_depth, MAXB) X(int, body_subtree_end, MAXB) X(int, level_start, MAXLEV + 1)      \
   X(int, level_body, MAXB) X(float, body_pos, MAXB * 3) X(float, body_quat, MAXB * 4)           \
   X(float, body_ipos, MAXB * 3) X(float, body_iquat, MAXB * 4) X(float, body_mass, MAXB)        \
   X(float, body_inertia, MAXB * 3) X(float, body_invweight0, MAXB * 2)                          \

@@ -48,27 +48,42 @@ AW_DEV void stage_kinematics(const DModel& m, Env& s, int lane) {
     s.xquat[0][0] = 1; s.xquat[0][1] = s.xquat[0][2] = s.xquat[0][3] = 0;
   }
   wsync();
+  // lane b owns body b (nbody <= 64) and works at its tree level; its model data (and its first
+  // joint's) are loaded once before the level sweep, so a level costs LDS reads of the parent
+  // frame + arithmetic, not a chain of dependent model loads
+  const bool own = lane > 0 && lane < m.nbody;
+  const int b = own ? lane : 0;
+  const int dep = own ? MD(body_depth, b) : -1;
+  const int p = MD(body_parentid, b), da = MD(body_dofadr, b), dn = own ? MD(body_dofnum, b) : 0;
+  float bp[3], bq[4], ax0[3], jp0[3];
+  for (int k = 0; k < 3; k++) bp[k] = MD(body_pos, 3 * b + k);
+  for (int k = 0; k < 4; k++) bq[k] = MD(body_quat, 4 * b + k);
+  if (own && MD(body_ovr, b)) { apply_ovr<3>(m, s, 0, b, bp); apply_ovr<4>(m, s, 1, b, bq); }
+  const int j0 = dn > 0 ? da : 0;
+  for (int q = 0; q < 3; q++) { ax0[q] = MD(jnt_axis, 3 * j0 + q); jp0[q] = MD(jnt_pos, 3 * j0 + q); }
+  const int jt0 = MD(jnt_type, j0);
   for (int lev = 1; lev < m.nlevel; lev++) {
-    int beg = MD(level_start, lev), end = MD(level_start, lev + 1);
-    for (int idx = beg + lane; idx < end; idx += 64) {
-      int b = MD(level_body, idx), p = MD(body_parentid, b);
-      float xp[3], xq[4], bp[3], bq[4], pq[4];
-      for (int k = 0; k < 3; k++) bp[k] = MD(body_pos, 3 * b + k);
-      for (int k = 0; k < 4; k++) { bq[k] = MD(body_quat, 4 * b + k); pq[k] = s.xquat[p][k]; }
-      if (MD(body_ovr, b)) { apply_ovr<3>(m, s, 0, b, bp); apply_ovr<4>(m, s, 1, b, bq); }
+    if (dep == lev) {
+      float xp[3], xq[4], pq[4];
+      for (int k = 0; k < 4; k++) pq[k] = s.xquat[p][k];
       rotvq(xp, bp, pq);
       add3(xp, xp, s.xpos[p]);
       mulq(xq, pq, bq);
-      int da = MD(body_dofadr, b);
-      for (int k = 0; k < MD(body_dofnum, b); k++) {
-        int j = da + k;
+      for (int k = 0; k < dn; k++) {
+        const int j = da + k;
         float axis[3], xaxis[3], xanchor[3], jp[3];
-        for (int q = 0; q < 3; q++) { axis[q] = MD(jnt_axis, 3 * j + q); jp[q] = MD(jnt_pos, 3 * j + q); }
+        int jt = jt0;
+        if (k == 0) {
+          for (int q = 0; q < 3; q++) { axis[q] = ax0[q]; jp[q] = jp0[q]; }
+        } else {
+          for (int q = 0; q < 3; q++) { axis[q] = MD(jnt_axis, 3 * j + q); jp[q] = MD(jnt_pos, 3 * j + q); }
+          jt = MD(jnt_type, j);
+        }
         rotvq(xaxis, axis, xq);
         rotvq(xanchor, jp, xq);
         add3(xanchor, xanchor, xp);
         float q = s.qpos[j];
-        if (MD(jnt_type, j) == JNT_SLIDE) {
+        if (jt == JNT_SLIDE) {
           for (int c = 0; c < 3; c++) xp[c] += xaxis[c] * q;
         } else {
           float sn, cs, ql[4], v[3];
@@ -226,23 +241,27 @@ AW_DEV float stage_velocity(const DModel& m, Env& s, int lane) {
     if (!(m.disableflags & DSBL_GRAVITY)) { cacc[0][3] = -m.gravity[0]; cacc[0][4] = -m.gravity[1]; cacc[0][5] = -m.gravity[2]; }
   }
   wsync();
-  for (int lev = 1; lev < m.nlevel; lev++) {
-    int beg = MD(level_start, lev), end = MD(level_start, lev + 1);
-    for (int idx = beg + lane; idx < end; idx += 64) {
-      int b = MD(level_body, idx), p = MD(body_parentid, b);
-      float cv[6], ca[6];
-      for (int k = 0; k < 6; k++) { cv[k] = cvel[p][k]; ca[k] = cacc[p][k]; }
-      int da = MD(body_dofadr, b);
-      for (int q = 0; q < MD(body_dofnum, b); q++) {
-        int j = da + q;
-        float cd[6], cdd[6], qv = s.qvel[j];
-        for (int k = 0; k < 6; k++) cd[k] = s.cdof[j][k];
-        cross_motion(cdd, cv, cd);
-        for (int k = 0; k < 6; k++) { cv[k] += cd[k] * qv; ca[k] += cdd[k] * qv; }
+  {
+    // lane b owns body b at its tree level (as in stage_kinematics)
+    const bool own = lane > 0 && lane < m.nbody;
+    const int b = own ? lane : 0;
+    const int dep = own ? MD(body_depth, b) : -1;
+    const int p = MD(body_parentid, b), da = MD(body_dofadr, b), dn = own ? MD(body_dofnum, b) : 0;
+    for (int lev = 1; lev < m.nlevel; lev++) {
+      if (dep == lev) {
+        float cv[6], ca[6];
+        for (int k = 0; k < 6; k++) { cv[k] = cvel[p][k]; ca[k] = cacc[p][k]; }
+        for (int q = 0; q < dn; q++) {
+          int j = da + q;
+          float cd[6], cdd[6], qv = s.qvel[j];
+          for (int k = 0; k < 6; k++) cd[k] = s.cdof[j][k];
+          cross_motion(cdd, cv, cd);
+          for (int k = 0; k < 6; k++) { cv[k] += cd[k] * qv; ca[k] += cdd[k] * qv; }
+        }
+        for (int k = 0; k < 6; k++) { cvel[b][k] = cv[k]; cacc[b][k] = ca[k]; }
       }
-      for (int k = 0; k < 6; k++) { cvel[b][k] = cv[k]; cacc[b][k] = ca[k]; }
+      wsync();
     }
-    wsync();
   }
   // local body force: cinert*cacc + cvel x* (cinert*cvel), written over cacc
   for (int b = 1 + lane; b < m.nbody; b += 64) {
