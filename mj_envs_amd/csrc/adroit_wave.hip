@@ -794,6 +794,21 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
     if (m.npairall > MAXDENSE * VS * 2) return fail(AW_EUNSUPPORTED, "too many collision pairs");
     PUT(cp_class, pcls); PUT(cp_rb, prb);
   }
+  {
+    std::vector<double> iw = B.f("body_invweight0");
+    std::vector<float> ptran(pg1.size()), prot(pg1.size());
+    std::vector<int> pr1(pg1.size()), pr2(pg1.size());
+    std::vector<unsigned long long> pm1(pg1.size()), pm2(pg1.size());
+    for (size_t p = 0; p < pg1.size(); p++) {
+      const int b1 = cbody[pg1[p]], b2 = cbody[pg2[p]];
+      ptran[p] = (float)iw[2 * b1] + (float)iw[2 * b2];
+      prot[p] = (float)iw[2 * b1 + 1] + (float)iw[2 * b2 + 1];
+      pr1[p] = rootid[b1]; pr2[p] = rootid[b2];
+      pm1[p] = bmask[b1]; pm2[p] = bmask[b2];
+    }
+    PUT(cp_tran, ptran); PUT(cp_rot, prot); PUT(cp_root1, pr1); PUT(cp_root2, pr2);
+    PUT(cp_mask1, pm1); PUT(cp_mask2, pm2);
+  }
   PUT(cp_g1, pg1); PUT(cp_g2, pg2); PUT(cp_condim, pcd); PUT(cp_friction, pfr);
   PUT(cp_solref, psr); PUT(cp_solimp, psi); PUT(cp_margin, pmg); PUT(cp_gap, pgp);
 

@@ -125,6 +125,10 @@ constexpr int MAXRG = 64;     // rendered (primitive) geoms
   X(float, cp_solimp, MAXPAIR * 5) X(float, cp_margin, MAXPAIR) X(float, cp_gap, MAXPAIR)       \
   /* broadphase: collider class of each pair, bounding radius sum (< 0: plane pair) */        \
   X(int, cp_class, MAXPAIR) X(float, cp_rb, MAXPAIR)                                           \
+  /* per-pair body data for the constraint rows (one model load per contact, not a chain) */    \
+  X(float, cp_tran, MAXPAIR) X(float, cp_rot, MAXPAIR) X(int, cp_root1, MAXPAIR)                \
+  X(int, cp_root2, MAXPAIR) X(unsigned long long, cp_mask1, MAXPAIR)                           \
+  X(unsigned long long, cp_mask2, MAXPAIR)                                                     \
   X(int, body_ovr, MAXB) X(int, site_ovr, MAXS) X(int, geom_ovr, MAXG) /* 1: overridden */    \
   X(int, task_idx, MAXTIDX) X(int, param_field, MAXP) X(int, param_obj, MAXP)                   \
   X(int, param_comp, MAXP) X(float, act_mid, MAXU) X(float, act_rng, MAXU)                      \

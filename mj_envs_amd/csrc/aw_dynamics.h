@@ -87,8 +87,10 @@ AW_DEV void stage_kinematics(const DModel& m, Env& s, int lane) {
           for (int c = 0; c < 3; c++) xp[c] += xaxis[c] * q;
         } else {
           float sn, cs, ql[4], v[3];
-          sn = sinf(0.5f * q);
-          cs = cosf(0.5f * q);
+          // hardware v_sin / v_cos (|q / 2| <= pi here): the library sinf / cosf pair was ~80 VALU
+          // per hinge on the level sweep's critical path
+          sn = __sinf(0.5f * q);
+          cs = __cosf(0.5f * q);
           ql[0] = cs; ql[1] = axis[0] * sn; ql[2] = axis[1] * sn; ql[3] = axis[2] * sn;
           mulq(xq, xq, ql);
           rotvq(v, jp, xq);

@@ -110,6 +110,7 @@ AW_DEV float getimpedance(const float* solimp, float pm) {
   if (x >= 1 || x <= 0) return x >= 1 ? dmax : d0;
   float y, mid = solimp[3], p = solimp[4];
   if (p == 1) y = x;
+  else if (p == 2) y = x <= mid ? x * x / mid : 1 - (1 - x) * (1 - x) / (1 - mid);   // default solimp power
   else if (x <= mid) y = powf(x, p) / powf(mid, p - 1);
   else y = 1 - powf(1 - x, p) / powf(1 - mid, p - 1);
   return d0 + y * (dmax - d0);
@@ -234,10 +235,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
   if (lane < ncon && !inc) atomicOr(&s.status, (unsigned)ST_EFC_OVERFLOW);
   if (lane < ncon) s.con_efc[lane] = inc ? nsparse + doff : -1;
   if (inc) {
-    int g1 = MD(cp_g1, pair), g2 = MD(cp_g2, pair);
-    int b1 = MD(geom_bodyid, g1), b2 = MD(geom_bodyid, g2);
-    float tran = MD(body_invweight0, 2 * b1) + MD(body_invweight0, 2 * b2);
-    float rot = MD(body_invweight0, 2 * b1 + 1) + MD(body_invweight0, 2 * b2 + 1);
+    const float tran = MD(cp_tran, pair), rot = MD(cp_rot, pair);
     float pm = s.con_dist[lane] - (MD(cp_margin, pair) - MD(cp_gap, pair));
     int r = nsparse + doff;
     if (dim == 1) {
@@ -257,30 +255,44 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
   }
   if (lane == 0) { s.nsparse = nsparse; s.ndense = nd; s.nefc = nsparse + nd; }
   wsync();
-  // dense J rows: one contact at a time, lane = dof
+  // dense J rows: one contact at a time, lane = dof.  The per-contact model data is gathered
+  // first with lane = contact (one round of loads) and broadcast with readlane in the loop.
+  unsigned long long c_m1 = 0ull, c_m2 = 0ull;
+  int c_root1 = 0, c_root2 = 0;
+  float c_f0 = 0.f, c_f1 = 0.f;
+  if (lane < ncon) {
+    c_m1 = MD(cp_mask1, pair); c_m2 = MD(cp_mask2, pair);
+    c_root1 = MD(cp_root1, pair); c_root2 = MD(cp_root2, pair);
+    c_f0 = MD(cp_friction, 5 * pair); c_f1 = MD(cp_friction, 5 * pair + 1);
+  }
+  const int c_pair = pair, c_dim = dim, c_r0 = lane < ncon ? s.con_efc[lane] : -1;
   for (int c = 0; c < ncon; c++) {
-    int r0 = s.con_efc[c];
+    const int r0 = rlane_i(c_r0, c);
     if (r0 < 0) break;
-    int pr = s.con_pair[c];
-    int cdim = MD(cp_condim, pr);
+    const int pr = rlane_i(c_pair, c);
+    const int cdim = rlane_i(c_dim, c);
     if (lane < NV) {
       int k = lane;
-      int b1 = MD(geom_bodyid, MD(cp_g1, pr)), b2 = MD(geom_bodyid, MD(cp_g2, pr));
+      const unsigned long long m1 = ((unsigned long long)(unsigned)rlane_i((int)(c_m1 >> 32), c) << 32) |
+                                    (unsigned)rlane_i((int)c_m1, c);
+      const unsigned long long m2 = ((unsigned long long)(unsigned)rlane_i((int)(c_m2 >> 32), c) << 32) |
+                                    (unsigned)rlane_i((int)c_m2, c);
+      const int root1 = rlane_i(c_root1, c), root2 = rlane_i(c_root2, c);
       const float* pos = s.con_pos[c];
       float fr[9];
       for (int q = 0; q < 3; q++) { fr[q] = s.con_nrm[c][q]; fr[3 + q] = 0.f; }
       make_frame(fr);
       const float* cd = s.cdof[k];
       float jp[3] = {0, 0, 0}, jr[3] = {0, 0, 0};
-      if ((MD(body_dofmask, b2) >> k) & 1ull) {
+      if ((m2 >> k) & 1ull) {
         float off3[3], t[3];
-        sub3(off3, pos, s.subcom[MD(body_rootid, b2)]);
+        sub3(off3, pos, s.subcom[root2]);
         cross3(t, cd, off3);
         for (int q = 0; q < 3; q++) { jr[q] += cd[q]; jp[q] += cd[3 + q] + t[q]; }
       }
-      if ((MD(body_dofmask, b1) >> k) & 1ull) {
+      if ((m1 >> k) & 1ull) {
         float off3[3], t[3];
-        sub3(off3, pos, s.subcom[MD(body_rootid, b1)]);
+        sub3(off3, pos, s.subcom[root1]);
         cross3(t, cd, off3);
         for (int q = 0; q < 3; q++) { jr[q] -= cd[q]; jp[q] -= cd[3 + q] + t[q]; }
       }
@@ -291,7 +303,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
         s.J[d][k] = B[0];
       } else {
         for (int kk = 1; kk < cdim; kk++) {
-          float fri = MD(cp_friction, 5 * pr + kk - 1);
+          const float fri = kk == 1 ? rlane(c_f0, c) : (kk == 2 ? rlane(c_f1, c) : MD(cp_friction, 5 * pr + kk - 1));
           s.J[d][k] = B[0] + fri * B[kk];
           s.J[d + 1][k] = B[0] - fri * B[kk];
           d += 2;
