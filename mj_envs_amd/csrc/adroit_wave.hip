@@ -91,20 +91,21 @@ AW_DEV void stage_collision(const DModel& m, Env& s, int lane) {
 #pragma unroll
     for (int c = 0; c < NCLASS; c++) cnt[c] = 0;
     const unsigned long long below = (1ull << lane) - 1ull;
-    for (int base = 0; base < m.npairall; base += 64) {
+    for (int base = 0; base < m.npairall; base += 64) {   // rounds of 64 pairs
       const int p = base + lane;
       bool pass = false;
       int cls = -1;
       if (p < m.npairall) {
-        cls = MD(cp_class, p);
+        const int pk = MD(cp_pack, p);
         const float rb = MD(cp_rb, p);
+        cls = pk & 0xff;
         if (rb < 0.f) {
           pass = true;
         } else {
-          const int g1 = MD(cp_g1, p), g2 = MD(cp_g2, p);
+          const int g1 = (pk >> 8) & 0xff, g2 = pk >> 16;
           float dif[3];
           sub3(dif, s.gxpos[g1], s.gxpos[g2]);
-          pass = !(norm3(dif) > rb);
+          pass = !(dot3(dif, dif) > rb * rb);
         }
       }
 #pragma unroll
@@ -793,6 +794,9 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
     for (int c = 0; c < NCLASS; c++) m.cls_start[c + 1] = m.cls_start[c] + ccount[c];
     if (m.npairall > MAXDENSE * VS * 2) return fail(AW_EUNSUPPORTED, "too many collision pairs");
     PUT(cp_class, pcls); PUT(cp_rb, prb);
+    std::vector<int> ppack(m.npairall);
+    for (int p = 0; p < m.npairall; p++) ppack[p] = pcls[p] | (pg1[p] << 8) | (pg2[p] << 16);
+    PUT(cp_pack, ppack);
   }
   {
     std::vector<double> iw = B.f("body_invweight0");

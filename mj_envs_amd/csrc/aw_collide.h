@@ -465,19 +465,21 @@ AW_DEV float sgn(float x) { return x < 0 ? -1.f : (x > 0 ? 1.f : 0.f); }
 
 struct Sup { float v[3], v1[3], v2[3]; };
 
+// support point of a primitive in direction dir (world), inflated by margin / 2.  Branch-free:
+// the lanes of one MPR round hold pairs of different geom types, and a type switch would run
+// every shape's branch in turn.
 AW_DEV void gsupport(float* res, const GV& g, const float* dir, float margin) {
   float ld[3], r[3];
   mulmtv3(ld, g.mat, dir);
   const float* s = g.size;
-  if (g.type == GEOM_SPHERE) { scl3(r, ld, s[0]); }
-  else if (g.type == GEOM_CAPSULE) { scl3(r, ld, s[0]); r[2] += sgn(ld[2]) * s[1]; }
-  else if (g.type == GEOM_CYLINDER) {
-    float tmp = sqrtf(ld[0] * ld[0] + ld[1] * ld[1]);
-    if (tmp > MINVAL) { r[0] = ld[0] / tmp * s[0]; r[1] = ld[1] / tmp * s[0]; }
-    else { r[0] = r[1] = 0; }
-    r[2] = sgn(ld[2]) * s[1];
-  } else if (g.type == GEOM_BOX) { for (int k = 0; k < 3; k++) r[k] = sgn(ld[k]) * s[k]; }
-  else { r[0] = r[1] = r[2] = 0; }
+  const bool box = g.type == GEOM_BOX, cyl = g.type == GEOM_CYLINDER, cap = g.type == GEOM_CAPSULE;
+  const bool round = g.type == GEOM_SPHERE || cap;
+  const float sg0 = sgn(ld[0]), sg1 = sgn(ld[1]), sg2 = sgn(ld[2]);
+  const float tmp = sqrtf(ld[0] * ld[0] + ld[1] * ld[1]);
+  const float ci = tmp > MINVAL ? s[0] / tmp : 0.f;
+  r[0] = box ? sg0 * s[0] : (cyl ? ld[0] * ci : (round ? ld[0] * s[0] : 0.f));
+  r[1] = box ? sg1 * s[1] : (cyl ? ld[1] * ci : (round ? ld[1] * s[0] : 0.f));
+  r[2] = box ? sg2 * s[2] : (cyl ? sg2 * s[1] : (round ? fmaf(ld[2], s[0], cap ? sg2 * s[1] : 0.f) : 0.f));
   for (int k = 0; k < 3; k++) r[k] += ld[k] * margin / 2;
   mulmv3(res, g.mat, r);
   add3(res, res, g.pos);

@@ -125,6 +125,7 @@ constexpr int MAXRG = 64;     // rendered (primitive) geoms
   X(float, cp_solimp, MAXPAIR * 5) X(float, cp_margin, MAXPAIR) X(float, cp_gap, MAXPAIR)       \
   /* broadphase: collider class of each pair, bounding radius sum (< 0: plane pair) */        \
   X(int, cp_class, MAXPAIR) X(float, cp_rb, MAXPAIR)                                           \
+  X(int, cp_pack, MAXPAIR) /* class | g1 << 8 | g2 << 16, one load per broadphase test */     \
   /* per-pair body data for the constraint rows (one model load per contact, not a chain) */    \
   X(float, cp_tran, MAXPAIR) X(float, cp_rot, MAXPAIR) X(int, cp_root1, MAXPAIR)                \
   X(int, cp_root2, MAXPAIR) X(unsigned long long, cp_mask1, MAXPAIR)                           \
