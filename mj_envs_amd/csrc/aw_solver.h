@@ -572,11 +572,14 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
     __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
+  // backward, right-looking: finish entry j, then eliminate it from entries k < j with row j
+  // of L (a contiguous, 16-byte aligned row: broadcast b128 reads; the left-looking form read
+  // the factor by columns, one b32 per entry)
   for (int j = NV - 1; j >= 0; j--) {
-    float acc = Mi[j];
+    Mi[j] *= s.vec2[j];
+    const float mj = Mi[j];
 #pragma unroll
-    for (int k = j + 1; k < NV; k++) acc = fmaf(-s.L[tri(k) + j], Mi[k], acc);
-    Mi[j] = acc * s.vec2[j];
+    for (int k = 0; k < j; k++) Mi[k] = fmaf(-s.L[tri(j) + k], mj, Mi[k]);
     __builtin_amdgcn_sched_barrier(0);
   }
   if (lane >= NV) {
