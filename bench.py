@@ -25,7 +25,8 @@ ENV_ID = "hammer-v0"
 
 
 def cpu_baseline(model_blob, env_id, budget_s=12.0):
-    """Oracle (fp64 restatement, OpenMP over envs) on the host cores: bounded sample."""
+    """Oracle (fp64 restatement, OpenMP over envs) on the host cores: bounded sample, all cores
+    (2/3 of the budget) and one core (1/3), BASELINE.md §2."""
     import numpy as np
     from mj_envs_amd.tasks import attach_task, load_model, sample_params
     from oracle.pyoracle import Oracle, build
@@ -35,19 +36,48 @@ def cpu_baseline(model_blob, env_id, budget_s=12.0):
     o.set_option(max_con=32, max_efc=128)
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     threads = max(1, min(threads, 16))
-    n = 64 * threads
-    rng = np.random.default_rng(0)
-    P = sample_params(env_id, m, rng, n)
-    st, _ = o.reset(P, nthreads=threads)
-    steps = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s:
-        o.step(st, rng.uniform(-1, 1, (n, o.nu)), nthreads=threads)
-        steps += 1
+
+    def run(nth, budget):
+        n = 64 * nth
+        rng = np.random.default_rng(0)
+        P = sample_params(env_id, m, rng, n)
+        st, _ = o.reset(P, nthreads=nth)
+        steps = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < budget:
+            o.step(st, rng.uniform(-1, 1, (n, o.nu)), nthreads=nth)
+            steps += 1
+        dt = time.perf_counter() - t0
+        return n * steps / dt, n, steps, dt
+
+    v, n, steps, dt = run(threads, budget_s * 2 / 3)
+    v1, n1, steps1, dt1 = run(1, budget_s / 3)
+    return dict(value=v, unit="env-steps/s", cores=threads, kind="port",
+                single_core_value=v1,
+                sample=f"{env_id}, {n} envs x {steps} env-steps (random policy) on {threads} threads in {dt:.1f} s "
+                       f"and {n1} envs x {steps1} env-steps on 1 thread in {dt1:.1f} s; fp64 C++ oracle "
+                       f"(restated mj_step + task layer), OpenMP over envs")
+
+
+def config2(blob, env_id, device, n=4096, steps=100, warmup=10):
+    """BASELINE configs[1] (hammer-v0, 4 096 envs, random policy) as an auxiliary figure."""
+    import torch
+    from mj_envs_amd import _native
+    sim = _native.Sim(blob, n, device=device)
+    obs, act = sim.empty(n, sim.obs_dim), sim.empty(n, sim.nu)
+    rew, done, goal = sim.empty(n), sim.empty(n, dtype=torch.uint8), sim.empty(n, dtype=torch.uint8)
+    sim.reset(obs, seed=7)
+    for k in range(warmup + steps):
+        if k == warmup:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        sim.random_actions(act, 0, k)
+        sim.step(act, obs, rew, done, goal, autoreset=True, seed=7)
+    torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    return dict(value=n * steps / dt, unit="env-steps/s", cores=threads, kind="port",
-                sample=f"{env_id}, {n} envs x {steps} env-steps (random policy), fp64 C++ oracle "
-                       f"(restated mj_step + task layer), OpenMP {threads} threads, {dt:.1f} s")
+    sim.close()
+    return dict(value=round(n * steps / dt, 1), unit="env-steps/s", envs=n, steps=steps,
+                ms_per_step=round(dt / steps * 1e3, 4))
 
 
 def pmc_traffic(env_per_launch):
@@ -199,6 +229,8 @@ def main():
                     config=dict(workload=workload, envs_per_gpu=n, total_envs=world * n,
                                 frame_skip=sim.frame_skip, parallelism=f"env-shard x{world}"),
                     roofline=roof, finite=finite)
+        if world == 1 and env_id == ENV_ID and depth is None and pol is None and n == 65536:
+            line["config2_4096_envs"] = config2(blob, env_id, local)
         if world == 1 and not args.no_cpu_baseline:
             try:
                 line["cpu_baseline"] = cpu_baseline(blob, env_id)
