@@ -448,47 +448,62 @@ AW_DEV void c_box_box(const GV& A, const GV& B, float margin, Emit& e) {
 // ---------------------------------------------------------------------------------------
 // MPR (libccd ccdMPRPenetration), supports inflated by margin/2 (mjccd_support)
 namespace mpr {
-constexpr float EPS = 1.1920928955078125e-07f;  // FLT_EPSILON (libccd CCD_EPS for float)
-AW_DEV bool is_zero(float x) { return fabsf(x) < EPS; }
-AW_DEV bool eq(float a, float b) {
-  float ab = fabsf(a - b);
+// Precision: fp32 by default (libccd's float build, CCD_EPS = FLT_EPSILON).  -DAW_MPR_FP64 runs
+// MPR in fp64 like MuJoCo's double libccd (CCD_EPS = DBL_EPSILON): that removes the rare fp32
+// failures on shallow face-on-face contacts (a cylinder lying on a box: the portal can settle on
+// a side face) -- tests/test_gpu_parity.py::test_hammer_variations_one_step -- at ~9 % of
+// k_step time (MI355X fp64 VALU at half the fp32 rate, twice the registers).
+#ifdef AW_MPR_FP64
+using real = double;
+constexpr real EPS = 2.220446049250313e-16;  // DBL_EPSILON
+#else
+using real = float;
+constexpr real EPS = 1.1920928955078125e-07f;  // FLT_EPSILON
+#endif
+struct GVd {
+  real pos[3], mat[9], size[3];
+  int type;
+};
+AW_DEV bool is_zero(real x) { return fabs(x) < EPS; }
+AW_DEV bool eq(real a, real b) {
+  real ab = fabs(a - b);
   if (ab < EPS) return true;
-  float fa = fabsf(a), fb = fabsf(b);
+  real fa = fabs(a), fb = fabs(b);
   return fb > fa ? ab < EPS * fb : ab < EPS * fa;
 }
-AW_DEV bool veq(const float* a, const float* b) { return eq(a[0], b[0]) && eq(a[1], b[1]) && eq(a[2], b[2]); }
-AW_DEV void vnorm(float* v) {
-  float k = 1.0f / sqrtf(dot3(v, v));
+AW_DEV bool veq(const real* a, const real* b) { return eq(a[0], b[0]) && eq(a[1], b[1]) && eq(a[2], b[2]); }
+AW_DEV void vnorm(real* v) {
+  real k = real(1.0) / sqrt(dot3(v, v));
   scl3(v, v, k);
 }
-AW_DEV float sgn(float x) { return x < 0 ? -1.f : (x > 0 ? 1.f : 0.f); }
+AW_DEV real sgn(real x) { return x < 0 ? -real(1.0) : (x > 0 ? real(1.0) : real(0.0)); }
 
-struct Sup { float v[3], v1[3], v2[3]; };
+struct Sup { real v[3], v1[3], v2[3]; };
 
 // support point of a primitive in direction dir (world), inflated by margin / 2.  Branch-free:
 // the lanes of one MPR round hold pairs of different geom types, and a type switch would run
 // every shape's branch in turn.
-AW_DEV void gsupport(float* res, const GV& g, const float* dir, float margin) {
-  float ld[3], r[3];
+AW_DEV void gsupport(real* res, const GVd& g, const real* dir, real margin) {
+  real ld[3], r[3];
   mulmtv3(ld, g.mat, dir);
-  const float* s = g.size;
+  const real* s = g.size;
   const bool box = g.type == GEOM_BOX, cyl = g.type == GEOM_CYLINDER, cap = g.type == GEOM_CAPSULE;
   const bool round = g.type == GEOM_SPHERE || cap;
-  const float sg0 = sgn(ld[0]), sg1 = sgn(ld[1]), sg2 = sgn(ld[2]);
-  const float tmp = sqrtf(ld[0] * ld[0] + ld[1] * ld[1]);
-  const float ci = tmp > MINVAL ? s[0] / tmp : 0.f;
-  r[0] = box ? sg0 * s[0] : (cyl ? ld[0] * ci : (round ? ld[0] * s[0] : 0.f));
-  r[1] = box ? sg1 * s[1] : (cyl ? ld[1] * ci : (round ? ld[1] * s[0] : 0.f));
-  r[2] = box ? sg2 * s[2] : (cyl ? sg2 * s[1] : (round ? fmaf(ld[2], s[0], cap ? sg2 * s[1] : 0.f) : 0.f));
+  const real sg0 = sgn(ld[0]), sg1 = sgn(ld[1]), sg2 = sgn(ld[2]);
+  const real tmp = sqrt(ld[0] * ld[0] + ld[1] * ld[1]);
+  const real ci = tmp > MINVAL ? s[0] / tmp : real(0.0);
+  r[0] = box ? sg0 * s[0] : (cyl ? ld[0] * ci : (round ? ld[0] * s[0] : real(0.0)));
+  r[1] = box ? sg1 * s[1] : (cyl ? ld[1] * ci : (round ? ld[1] * s[0] : real(0.0)));
+  r[2] = box ? sg2 * s[2] : (cyl ? sg2 * s[1] : (round ? fma(ld[2], s[0], cap ? sg2 * s[1] : real(0.0)) : real(0.0)));
   for (int k = 0; k < 3; k++) r[k] += ld[k] * margin / 2;
   mulmv3(res, g.mat, r);
   add3(res, res, g.pos);
 }
 
-struct Ctx { const GV* g1; const GV* g2; float margin, tol; int maxit; };
+struct Ctx { const GVd* g1; const GVd* g2; real margin, tol; int maxit; };
 
-AW_DEV void support(const Ctx& c, const float* dir, Sup& s) {
-  float nd[3];
+AW_DEV void support(const Ctx& c, const real* dir, Sup& s) {
+  real nd[3];
   scl3(nd, dir, -1);
   gsupport(s.v1, *c.g1, dir, c.margin);
   gsupport(s.v2, *c.g2, nd, c.margin);
@@ -502,16 +517,16 @@ AW_DEV void setsup(Sup& d, const Sup& s) {
   for (int k = 0; k < 3; k++) { d.v[k] = s.v[k]; d.v1[k] = s.v1[k]; d.v2[k] = s.v2[k]; }
 }
 
-AW_DEV void portal_dir(const Portal& P, float* dir) {
-  float a[3], b[3];
+AW_DEV void portal_dir(const Portal& P, real* dir) {
+  real a[3], b[3];
   sub3(a, P.p2.v, P.p1.v);
   sub3(b, P.p3.v, P.p1.v);
   cross3(dir, a, b);
   vnorm(dir);
 }
-AW_DEV bool reach_tol(const Portal& P, const Sup& v4, const float* dir, float tol) {
-  float dv1 = dot3(P.p1.v, dir), dv2 = dot3(P.p2.v, dir), dv3 = dot3(P.p3.v, dir), dv4 = dot3(v4.v, dir);
-  float d1 = fminf(fminf(dv4 - dv1, dv4 - dv2), dv4 - dv3);
+AW_DEV bool reach_tol(const Portal& P, const Sup& v4, const real* dir, real tol) {
+  real dv1 = dot3(P.p1.v, dir), dv2 = dot3(P.p2.v, dir), dv3 = dot3(P.p3.v, dir), dv4 = dot3(v4.v, dir);
+  real d1 = fmin(fmin(dv4 - dv1, dv4 - dv2), dv4 - dv3);
   return eq(d1, tol) || d1 < tol;
 }
 AW_DEV void selsup(Sup& d, bool c, const Sup& s) {
@@ -523,7 +538,7 @@ AW_DEV void selsup(Sup& d, bool c, const Sup& s) {
 // branch-free vertex replacement: conditional struct stores through a selected pointer would
 // pin the portal in scratch
 AW_DEV void expand(Portal& P, const Sup& v4) {
-  float v4v0[3];
+  real v4v0[3];
   cross3(v4v0, v4.v, P.p0.v);
   const bool a1 = dot3(P.p1.v, v4v0) > 0;
   const bool a2 = dot3(P.p2.v, v4v0) > 0;
@@ -533,16 +548,16 @@ AW_DEV void expand(Portal& P, const Sup& v4) {
   selsup(P.p2, !a1 && a3, v4);
 }
 AW_DEV int discover(const Ctx& c, Portal& P) {
-  float dir[3], va[3], vb[3];
+  real dir[3], va[3], vb[3];
   copy3(P.p0.v1, c.g1->pos);
   copy3(P.p0.v2, c.g2->pos);
   sub3(P.p0.v, P.p0.v1, P.p0.v2);
-  const float zero[3] = {0, 0, 0};
+  const real zero[3] = {0, 0, 0};
   if (veq(P.p0.v, zero)) P.p0.v[0] += EPS * 10;
   scl3(dir, P.p0.v, -1);
   vnorm(dir);
   support(c, dir, P.p1);
-  float d = dot3(P.p1.v, dir);
+  real d = dot3(P.p1.v, dir);
   if (is_zero(d) || d < 0) return -1;
   cross3(dir, P.p0.v, P.p1.v);
   if (is_zero(dot3(dir, dir))) return veq(P.p1.v, zero) ? 1 : 2;
@@ -583,26 +598,26 @@ AW_DEV int discover(const Ctx& c, Portal& P) {
   return -1;
 }
 AW_DEV int refine(const Ctx& c, Portal& P) {
-  float dir[3];
+  real dir[3];
   Sup v4;
   for (int it = 0; it <= c.maxit; it++) {
     portal_dir(P, dir);
-    float d = dot3(dir, P.p1.v);
+    real d = dot3(dir, P.p1.v);
     if (is_zero(d) || d > 0) return 0;
     support(c, dir, v4);
-    float d4 = dot3(v4.v, dir);
+    real d4 = dot3(v4.v, dir);
     if (!(is_zero(d4) || d4 > 0) || reach_tol(P, v4, dir, c.tol)) return -1;
     expand(P, v4);
   }
   return -1;
 }
-AW_DEV float pseg2(const float* P, const float* x0, const float* b, float* w) {
-  float dd[3], a[3];
+AW_DEV real pseg2(const real* P, const real* x0, const real* b, real* w) {
+  real dd[3], a[3];
   sub3(dd, b, x0);
   sub3(a, x0, P);
-  float t = -dot3(a, dd) / dot3(dd, dd);
+  real t = -dot3(a, dd) / dot3(dd, dd);
   const bool lo = t < 0 || is_zero(t), hi = !lo && (t > 1 || eq(t, 1));
-  float df[3];
+  real df[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     w[k] = lo ? x0[k] : (hi ? b[k] : x0[k] + dd[k] * t);
@@ -610,25 +625,25 @@ AW_DEV float pseg2(const float* P, const float* x0, const float* b, float* w) {
   }
   return dot3(df, df);
 }
-AW_DEV float ptri2(const float* P, const float* x0, const float* B, const float* C, float* w) {
-  float d1[3], d2[3], a[3];
+AW_DEV real ptri2(const real* P, const real* x0, const real* B, const real* C, real* w) {
+  real d1[3], d2[3], a[3];
   sub3(d1, B, x0);
   sub3(d2, C, x0);
   sub3(a, x0, P);
-  float v = dot3(d1, d1), ww = dot3(d2, d2), p = dot3(a, d1), q = dot3(a, d2), r = dot3(d1, d2);
-  float dd = ww * v - r * r, s, t;
+  real v = dot3(d1, d1), ww = dot3(d2, d2), p = dot3(a, d1), q = dot3(a, d2), r = dot3(d1, d2);
+  real dd = ww * v - r * r, s, t;
   if (is_zero(dd)) { s = t = -1; }
   else { s = (q * r - ww * p) / dd; t = (-s * r - q) / ww; }
   if ((is_zero(s) || s > 0) && (eq(s, 1) || s < 1) && (is_zero(t) || t > 0) && (eq(t, 1) || t < 1) &&
       (eq(t + s, 1) || t + s < 1)) {
     for (int k = 0; k < 3; k++) w[k] = x0[k] + d1[k] * s + d2[k] * t;
-    float df[3];
+    real df[3];
     sub3(df, w, P);
     return dot3(df, df);
   }
-  float w2[3];
-  float dist = pseg2(P, x0, B, w);
-  float d2s = pseg2(P, x0, C, w2);
+  real w2[3];
+  real dist = pseg2(P, x0, B, w);
+  real d2s = pseg2(P, x0, C, w2);
   bool take = d2s < dist;
   dist = take ? d2s : dist;
 #pragma unroll
@@ -640,14 +655,14 @@ AW_DEV float ptri2(const float* P, const float* x0, const float* B, const float*
   for (int k = 0; k < 3; k++) w[k] = take ? w2[k] : w[k];
   return dist;
 }
-AW_DEV void find_pos(const Portal& P, float* pos) {
-  float dir[3], vec[3], b0, b1, b2, b3;
+AW_DEV void find_pos(const Portal& P, real* pos) {
+  real dir[3], vec[3], b0, b1, b2, b3;
   portal_dir(P, dir);
   cross3(vec, P.p1.v, P.p2.v); b0 = dot3(vec, P.p3.v);
   cross3(vec, P.p3.v, P.p2.v); b1 = dot3(vec, P.p0.v);
   cross3(vec, P.p0.v, P.p1.v); b2 = dot3(vec, P.p3.v);
   cross3(vec, P.p2.v, P.p1.v); b3 = dot3(vec, P.p0.v);
-  float sum = b0 + b1 + b2 + b3;
+  real sum = b0 + b1 + b2 + b3;
   if (is_zero(sum) || sum < 0) {
     b0 = 0;
     cross3(vec, P.p2.v, P.p3.v); b1 = dot3(vec, dir);
@@ -655,40 +670,40 @@ AW_DEV void find_pos(const Portal& P, float* pos) {
     cross3(vec, P.p1.v, P.p2.v); b3 = dot3(vec, dir);
     sum = b1 + b2 + b3;
   }
-  float inv = 1.0f / sum;
+  real inv = real(1.0) / sum;
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    float p1 = P.p0.v1[k] * b0 + P.p1.v1[k] * b1 + P.p2.v1[k] * b2 + P.p3.v1[k] * b3;
-    float p2 = P.p0.v2[k] * b0 + P.p1.v2[k] * b1 + P.p2.v2[k] * b2 + P.p3.v2[k] * b3;
-    pos[k] = 0.5f * (p1 + p2) * inv;
+    real p1 = P.p0.v1[k] * b0 + P.p1.v1[k] * b1 + P.p2.v1[k] * b2 + P.p3.v1[k] * b3;
+    real p2 = P.p0.v2[k] * b0 + P.p1.v2[k] * b1 + P.p2.v2[k] * b2 + P.p3.v2[k] * b3;
+    pos[k] = real(0.5) * (p1 + p2) * inv;
   }
 }
-AW_DEV int penetration(const Ctx& c, float* depth, float* dir, float* pos) {
+AW_DEV int penetration(const Ctx& c, real* depth, real* dir, real* pos) {
   Portal P;
   int res = discover(c, P);
   if (res < 0) return -1;
   if (res == 1) {
     *depth = 0;
     dir[0] = dir[1] = dir[2] = 0;
-    for (int k = 0; k < 3; k++) pos[k] = 0.5f * (P.p1.v1[k] + P.p1.v2[k]);
+    for (int k = 0; k < 3; k++) pos[k] = real(0.5) * (P.p1.v1[k] + P.p1.v2[k]);
     return 0;
   }
   if (res == 2) {
-    for (int k = 0; k < 3; k++) pos[k] = 0.5f * (P.p1.v1[k] + P.p1.v2[k]);
+    for (int k = 0; k < 3; k++) pos[k] = real(0.5) * (P.p1.v1[k] + P.p1.v2[k]);
     copy3(dir, P.p1.v);
-    *depth = sqrtf(dot3(dir, dir));
+    *depth = sqrt(dot3(dir, dir));
     vnorm(dir);
     return 0;
   }
   if (refine(c, P) < 0) return -1;
   Sup v4;
-  float pd[3];
+  real pd[3];
   for (int it = 0;; it++) {
     portal_dir(P, pd);
     support(c, pd, v4);
     if (reach_tol(P, v4, pd, c.tol) || it > c.maxit) {
-      const float zero[3] = {0, 0, 0};
-      *depth = sqrtf(ptri2(zero, P.p1.v, P.p2.v, P.p3.v, dir));
+      const real zero[3] = {0, 0, 0};
+      *depth = sqrt(ptri2(zero, P.p1.v, P.p2.v, P.p3.v, dir));
       if (is_zero(*depth)) dir[0] = dir[1] = dir[2] = 0;
       else vnorm(dir);
       find_pos(P, pos);
@@ -700,13 +715,19 @@ AW_DEV int penetration(const Ctx& c, float* depth, float* dir, float* pos) {
 }  // namespace mpr
 
 AW_DEV void c_convex(const DModel& m, const GV& a, const GV& b, float margin, Emit& e) {
-  mpr::Ctx ctx{&a, &b, margin, m.mpr_tolerance, m.mpr_iterations};
-  float depth, dir[3], pos[3];
+  mpr::GVd ad, bd;
+  for (int k = 0; k < 3; k++) { ad.pos[k] = a.pos[k]; ad.size[k] = a.size[k]; bd.pos[k] = b.pos[k]; bd.size[k] = b.size[k]; }
+  for (int k = 0; k < 9; k++) { ad.mat[k] = a.mat[k]; bd.mat[k] = b.mat[k]; }
+  ad.type = a.type; bd.type = b.type;
+  mpr::Ctx ctx{&ad, &bd, (mpr::real)margin, (mpr::real)m.mpr_tolerance, m.mpr_iterations};
+  mpr::real depth, dir[3], pos[3];
   if (mpr::penetration(ctx, &depth, dir, pos) != 0) return;
   if (dir[0] == 0 && dir[1] == 0 && dir[2] == 0) return;
-  float dist = margin - depth;
+  const float dist = margin - (float)depth;
   if (dist > margin) return;
-  emit(e, dist, pos, dir);
+  const float pf[3] = {(float)pos[0], (float)pos[1], (float)pos[2]};
+  const float df[3] = {(float)dir[0], (float)dir[1], (float)dir[2]};
+  emit(e, dist, pf, df);
 }
 
 // ---------------------------------------------------------------------------------------

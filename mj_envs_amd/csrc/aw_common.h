@@ -346,6 +346,29 @@ AW_DEV void normq(float* q) {
 }
 AW_DEV float clampf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
+// fp64 overloads of the 3D helpers (MPR runs in double: aw_collide.h)
+AW_DEV double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+AW_DEV void cross3(double* r, const double* a, const double* b) {
+  double t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+AW_DEV void sub3(double* r, const double* a, const double* b) { r[0] = a[0] - b[0]; r[1] = a[1] - b[1]; r[2] = a[2] - b[2]; }
+AW_DEV void add3(double* r, const double* a, const double* b) { r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2]; }
+AW_DEV void scl3(double* r, const double* a, double s) { r[0] = a[0] * s; r[1] = a[1] * s; r[2] = a[2] * s; }
+AW_DEV void copy3(double* r, const double* a) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; }
+AW_DEV void mulmv3(double* r, const double* m, const double* v) {
+  double t0 = m[0] * v[0] + m[1] * v[1] + m[2] * v[2];
+  double t1 = m[3] * v[0] + m[4] * v[1] + m[5] * v[2];
+  double t2 = m[6] * v[0] + m[7] * v[1] + m[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+AW_DEV void mulmtv3(double* r, const double* m, const double* v) {
+  double t0 = m[0] * v[0] + m[3] * v[1] + m[6] * v[2];
+  double t1 = m[1] * v[0] + m[4] * v[1] + m[7] * v[2];
+  double t2 = m[2] * v[0] + m[5] * v[1] + m[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+
 // mju_makeFrame
 AW_DEV void make_frame(float* f) {
   normalize3(f);
