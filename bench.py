@@ -103,6 +103,8 @@ def main():
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--envs-per-gpu", type=int, default=65536)
+    ap.add_argument("--total-envs", type=int, default=0,
+                    help="strong scaling: fixed total envs split over the ranks (e.g. 262144, SURVEY C4)")
     ap.add_argument("--env", default=ENV_ID)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--policy", action="store_true",
@@ -119,6 +121,11 @@ def main():
 
     if args.depth and args.envs_per_gpu == 65536:
         args.envs_per_gpu = 8192
+    if args.total_envs:
+        w = int(os.environ.get("WORLD_SIZE", "1"))
+        if args.total_envs % w:
+            raise SystemExit("--total-envs must divide evenly over the ranks")
+        args.envs_per_gpu = args.total_envs // w
     shard = shard_from_env(args.envs_per_gpu)
     world, rank, local = shard.world, shard.rank, shard.local_rank
     if world > 1:
@@ -224,7 +231,8 @@ def main():
         line = dict(metric=metric,
                     value=round(value, 1), unit="env-steps/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(elapsed / args.steps * 1e3, 4),
-                    higher_is_better=True, scaling="weak", vs_baseline=None, dtype="f32",
+                    higher_is_better=True, scaling="strong" if args.total_envs else "weak", vs_baseline=None,
+                    dtype="f32",
                     data="synthetic (Philox U(-1,1) actions, reference reset distribution)",
                     config=dict(workload=workload, envs_per_gpu=n, total_envs=world * n,
                                 frame_skip=sim.frame_skip, parallelism=f"env-shard x{world}"),
