@@ -522,13 +522,10 @@ __global__ void __launch_bounds__(256) k_depth(DModel m, DState st, int n, CamRe
     stage_kinematics(m, s, lane);
   }
   __syncthreads();
-  render_geoms(m, s, rg, tid, 256);
+  render_geoms(m, s, rg, cam.c, tid, 256);
   __syncthreads();
   float* o = out + (size_t)env * W * H;
-  for (int p = tid; p < W * H; p += 256) {
-    const int row = p / W, col = p - row * W;
-    o[p] = render_pixel(rg, m.nrgeom, cam.c, row, col);
-  }
+  for (int p0 = (tid >> 6) * 64; p0 < W * H; p0 += 256) render_span(rg, m.nrgeom, cam.c, W, H, p0, lane, o);
 }
 
 __global__ void k_random_actions(int n, int nu, uint64_t seed, uint64_t step, float* out) {

@@ -12,8 +12,9 @@ The reference renders RGB through OpenGL from mujoco-py's offscreen free camera
   zoom") and, with ``enable_resize``, resized to 64x64.
 
 The build replaces the GL rasteriser with a HIP ray caster (``aw_render_depth``): one
-workgroup per env, forward kinematics of the env's qpos on one wave, then every thread casts
-the rays of its pixels against every primitive geom.  The output is metric z-depth on the
+workgroup per env, forward kinematics of the env's qpos on one wave, then each geom's pixel
+box (its projected bounding sphere); each wave takes 64 pixels, ballots the geoms whose box
+meets those rows and casts its rays against only those.  The output is metric z-depth on the
 64x64 grid whose pixels are the 2x2 blocks of that 128x128 crop.  Depth has no reference
 counterpart (the reference returns RGB), so this path is parity-unpinned against the
 reference; it is checked against an independent numpy ray caster on the fp64 oracle's
