@@ -109,6 +109,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--policy", action="store_true",
                     help="closed loop: actions from the on-device Gaussian MLP (mjrl MLP, 32x32) instead of i.i.d.")
+    ap.add_argument("--mpr", choices=("task", "fp32", "fp64"), default="task",
+                    help="precision of the MPR (cylinder) collider: the task's default (tasks.py "
+                         "TaskSpec.mpr_fp64; hammer fp32), or forced")
     ap.add_argument("--depth", action="store_true",
                     help="BASELINE config 5: + 64x64 depth-camera obs every env-step (default 8192 envs)")
     args = ap.parse_args()
@@ -117,7 +120,7 @@ def main():
     import torch.distributed as dist
     from mj_envs_amd import _native, perfmodel
     from mj_envs_amd.dist import EpisodeGather, rank_seed, shard_from_env
-    from mj_envs_amd.tasks import attach_task, load_model
+    from mj_envs_amd.tasks import TASKS, attach_task, load_model
 
     if args.depth and args.envs_per_gpu == 65536:
         args.envs_per_gpu = 8192
@@ -139,6 +142,9 @@ def main():
     blob = m.to_blob()
     n = args.envs_per_gpu
     sim = _native.Sim(blob, n, device=local)
+    if args.mpr != "task":
+        sim.set_option(disableflags=_native.DSBL_MPR_FP64 if args.mpr == "fp32" else _native.DSBL_MPR_FP32)
+    mpr64 = args.mpr == "fp64" or (args.mpr == "task" and TASKS[env_id].mpr_fp64)
     obs = sim.empty(n, sim.obs_dim)
     act = sim.empty(n, sim.nu)
     rew = sim.empty(n)
@@ -225,6 +231,7 @@ def main():
             workload = (f"{env_id} + 64x64 depth-camera obs (HIP ray caster, BASELINE config 5), {n} envs per "
                         f"GPU, random policy, auto-reset at horizon {sim.horizon}")
             roof["depth_kernel_ms"] = round(depth_ms, 4)
+        workload += ", MPR collider in " + ("fp64" if mpr64 else "fp32")
         metric = "env-steps/sec at N parallel envs, hammer-v0, 1/2/4/8 MI355X"
         if env_id != "hammer-v0":   # BASELINE config 3 lines are labelled with their own task
             metric = f"env-steps/sec at N parallel envs, {env_id}, 1/2/4/8 MI355X"
@@ -237,7 +244,7 @@ def main():
                     config=dict(workload=workload, envs_per_gpu=n, total_envs=world * n,
                                 frame_skip=sim.frame_skip, parallelism=f"env-shard x{world}"),
                     roofline=roof, finite=finite)
-        if world == 1 and env_id == ENV_ID and depth is None and pol is None and n == 65536:
+        if world == 1 and env_id == ENV_ID and depth is None and pol is None and n == 65536 and args.mpr == "task":
             line["config2_4096_envs"] = config2(blob, env_id, local)
         if world == 1 and not args.no_cpu_baseline:
             try:

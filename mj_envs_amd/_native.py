@@ -18,6 +18,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AW_LIB") or os.path.join(HERE, "libadroit_hip.so")
 
 AW_NDIMS = 13
+# aw_set_option bits of ours: MPR (cylinder) collider in fp32 / in fp64 (neither: the task default)
+DSBL_MPR_FP64 = 1 << 16
+DSBL_MPR_FP32 = 1 << 17
 AW_DUMP_SIZE = 2728
 # float offsets inside the aw_forward_dump output (see adroit_wave.hip k_dump)
 DUMP_LAYOUT = dict(xpos=(0, 96), xquat=(96, 128), site_xpos=(224, 96), qacc_smooth=(320, 36),

@@ -72,16 +72,18 @@ AW_DEV void sort_contacts(Env& s, int lane) {
 }
 
 // narrowphase over the broadphase survivors of one collider class
-template <int C>
+template <int C, int MP>
 AW_DEV void narrow_class(const DModel& m, Env& s, const short* plist, int cnt, int lane) {
   const int st = m.cls_start[C];
-  for (int i = lane; i < cnt; i += 64) collide_pair<C>(m, s, plist[st + i]);
+  for (int i = lane; i < cnt; i += 64) collide_pair<C, MP>(m, s, plist[st + i]);
 }
 
 // mj_collision: bounding-sphere broadphase over the static candidate list (one pair per lane,
 // 64 per round), survivors compacted class-major into an LDS list (ballot + mbcnt), then ONE
 // narrowphase loop over the list: lanes of a round mostly share a collider, instead of every
 // round executing every collider branch its lanes happen to need.
+// MP: precision of the MPR collider (MPR_FP32 / MPR_FP64), a kernel template parameter
+template <int MP>
 AW_DEV void stage_collision(const DModel& m, Env& s, int lane) {
   if (lane == 0) s.ncon = 0;
   wsync();
@@ -118,15 +120,15 @@ AW_DEV void stage_collision(const DModel& m, Env& s, int lane) {
     }
     AW_PROF(s, PR_CO_BROAD);
     wsync();
-    narrow_class<0>(m, s, plist, cnt[0], lane);
+    narrow_class<0, MP>(m, s, plist, cnt[0], lane);
     AW_PROF(s, PR_CO_C0);
-    narrow_class<1>(m, s, plist, cnt[1], lane);
+    narrow_class<1, MP>(m, s, plist, cnt[1], lane);
     AW_PROF(s, PR_CO_C1);
-    narrow_class<2>(m, s, plist, cnt[2], lane);
+    narrow_class<2, MP>(m, s, plist, cnt[2], lane);
     AW_PROF(s, PR_CO_C2);
-    narrow_class<3>(m, s, plist, cnt[3], lane);
+    narrow_class<3, MP>(m, s, plist, cnt[3], lane);
     AW_PROF(s, PR_CO_C3);
-    narrow_class<4>(m, s, plist, cnt[4], lane);
+    narrow_class<4, MP>(m, s, plist, cnt[4], lane);
   }
   wsync();
   AW_PROF(s, PR_CO_NARROW);
@@ -141,11 +143,11 @@ struct Dof {
 // mj_forward: everything up to qacc / forces / sensors; Mrow is left in registers.  Stage order
 // follows the LDS overlays (aw_common.h Env): the constraint rows are assembled while the
 // phase-K arrays (cdof, subcom) are alive, then the solver phase reuses that storage.
-template <int NV>
+template <int NV, int MP>
 AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV], Dof& d) {
   stage_kinematics(m, s, lane);
   AW_PROF(s, PR_KIN);
-  stage_collision(m, s, lane);
+  stage_collision<MP>(m, s, lane);
   AW_PROF(s, PR_COLL);
   stage_com(m, s, lane);
   AW_PROF(s, PR_COM);
@@ -298,13 +300,13 @@ AW_DEV void reset_prepare(const DModel& m, Env& s, const DState& st, int env, in
 }
 
 // reset one env in LDS: params (given or sampled), qpos0/0/0, forward, obs
-template <int NV>
+template <int NV, int MP>
 AW_DEV void reset_env(const DModel& m, Env& s, const DState& st, int env, int lane,
                       const float* params_in, uint64_t seed, float* obs) {
   reset_prepare<NV>(m, s, st, env, lane, params_in, seed);
   float Mrow[NV];
   Dof d;
-  forward<NV>(m, s, lane, Mrow, d);
+  forward<NV, MP>(m, s, lane, Mrow, d);
   if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
 }
 
@@ -312,7 +314,7 @@ AW_DEV void reset_env(const DModel& m, Env& s, const DState& st, int env, int la
 // in-kernel auto-reset.  forward<NV> has exactly ONE inlined call site (the loop below drives
 // substeps, the mj_checkAcc retry and the reset forward through it), which keeps the code
 // object small enough for the instruction cache.
-template <int NV>
+template <int NV, int MP>
 __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel m, DState st, int n, const float* __restrict__ actions,
                                              float* obs, float* reward, uint8_t* done, uint8_t* goal,
                                              float* terminal_obs, int autoreset, uint64_t seed) {
@@ -339,7 +341,7 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel m, DState st, 
     asm volatile("" ::: "memory");
     if (!resetting && !retry) check_state<NV>(s, lane);
     AW_PROF(s, PR_CHECK);
-    forward<NV>(m, s, lane, Mrow, d);
+    forward<NV, MP>(m, s, lane, Mrow, d);
     if (resetting) break;
     if (!retry && check_acc<NV>(s, lane, d)) { retry = true; continue; }
     retry = false;
@@ -397,7 +399,7 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel m, DState st, 
 #endif
 }
 
-template <int NV>
+template <int NV, int MP>
 __global__ void __launch_bounds__(64) k_reset(DModel m, DState st, int n, const uint8_t* mask,
                                               const float* params, uint64_t seed, float* obs) {
   __shared__ Env s;
@@ -405,11 +407,11 @@ __global__ void __launch_bounds__(64) k_reset(DModel m, DState st, int n, const 
   if (env >= n) return;
   if (mask && !mask[env]) return;
   if (lane == 0) s.status = 0u;
-  reset_env<NV>(m, s, st, env, lane, params, seed, obs);
+  reset_env<NV, MP>(m, s, st, env, lane, params, seed, obs);
   store_env<NV>(m, s, st, env, lane);
 }
 
-template <int NV>
+template <int NV, int MP>
 __global__ void __launch_bounds__(64) k_set_state(DModel m, DState st, int n, const float* qpos,
                                                   const float* qvel, const float* warm,
                                                   const float* params, float* obs) {
@@ -429,13 +431,13 @@ __global__ void __launch_bounds__(64) k_set_state(DModel m, DState st, int n, co
   stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
   float Mrow[NV];
   Dof d;
-  forward<NV>(m, s, lane, Mrow, d);
+  forward<NV, MP>(m, s, lane, Mrow, d);
   if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
   store_env<NV>(m, s, st, env, lane);
 }
 
 // dump layout (floats): see mj_envs_amd/_native.py DUMP_LAYOUT
-template <int NV>
+template <int NV, int MP>
 __global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const float* ctrl, float* out) {
   __shared__ Env s;
   const int lane = threadIdx.x;
@@ -444,7 +446,7 @@ __global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const
   stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
   float Mrow[NV];
   Dof d;
-  forward<NV>(m, s, lane, Mrow, d);
+  forward<NV, MP>(m, s, lane, Mrow, d);
   for (int i = lane; i < MAXB * 3; i += 64) out[i] = i < m.nbody * 3 ? (&s.xpos[0][0])[i] : 0.f;
   for (int i = lane; i < MAXB * 4; i += 64) out[96 + i] = i < m.nbody * 4 ? (&s.xquat[0][0])[i] : 0.f;
   for (int i = lane; i < MAXS * 3; i += 64) out[224 + i] = i < m.nsite * 3 ? (&s.sxpos[0][0])[i] : 0.f;
@@ -585,6 +587,7 @@ std::vector<float> tof(const std::vector<double>& v) { return std::vector<float>
 
 struct aw_handle {
   int device, nenv, NV;
+  int mpr_fp64;   // the task's MPR collider precision (blob task_mpr_fp64); see mpr_kernel_fp64()
   DModel m;
   DState st;
   void* dmodel = nullptr;
@@ -871,30 +874,38 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
   return AW_OK;
 }
 
-template <int NV>
+template <int NV, int MP>
 static void launch_step(aw_handle* h, const float* a, float* obs, float* rew, uint8_t* done, uint8_t* goal,
                         float* tobs, int autoreset, uint64_t seed, hipStream_t st) {
-  hipLaunchKernelGGL((k_step<NV>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, a, obs, rew, done,
+  hipLaunchKernelGGL((k_step<NV, MP>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, a, obs, rew, done,
                      goal, tobs, autoreset, seed);
 }
-template <int NV>
+template <int NV, int MP>
 static void launch_reset(aw_handle* h, const uint8_t* mask, const float* params, uint64_t seed, float* obs,
                          hipStream_t st) {
-  hipLaunchKernelGGL((k_reset<NV>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, mask, params, seed, obs);
+  hipLaunchKernelGGL((k_reset<NV, MP>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, mask, params, seed, obs);
 }
-template <int NV>
+template <int NV, int MP>
 static void launch_set(aw_handle* h, const float* q, const float* v, const float* w, const float* p, float* obs,
                        hipStream_t st) {
-  hipLaunchKernelGGL((k_set_state<NV>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, q, v, w, p, obs);
+  hipLaunchKernelGGL((k_set_state<NV, MP>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, q, v, w, p, obs);
 }
-template <int NV>
+template <int NV, int MP>
 static void launch_dump(aw_handle* h, int env, const float* ctrl, float* out, hipStream_t st) {
-  hipLaunchKernelGGL((k_dump<NV>), dim3(1), dim3(64), 0, st, h->m, h->st, env, ctrl, out);
+  hipLaunchKernelGGL((k_dump<NV, MP>), dim3(1), dim3(64), 0, st, h->m, h->st, env, ctrl, out);
 }
 
 template <int NV>
 static void launch_depth(aw_handle* h, const CamRec& cam, int W, int H, float* out, hipStream_t st) {
   hipLaunchKernelGGL((k_depth<NV>), dim3(h->nenv), dim3(256), 0, st, h->m, h->st, h->nenv, cam, W, H, out);
+}
+
+// MPR precision of the forward kernels (template parameter MP): the task default unless a
+// disable bit forces one (include/adroit_wave.h aw_set_option)
+static bool mpr_kernel_fp64(const aw_handle* h) {
+  if (h->m.disableflags & DSBL_MPR_FP64) return false;
+  if (h->m.disableflags & DSBL_MPR_FP32) return true;
+  return h->mpr_fp64 != 0;
 }
 
 #ifdef AW_ONLY_NV
@@ -927,6 +938,7 @@ int aw_create(const void* blob, size_t nbytes, int n_envs, int device, aw_handle
   int rc = build_model(B, h->m, *md);
   if (rc) { delete h; return rc; }
   h->NV = h->m.nv;
+  h->mpr_fp64 = B.dim("task_mpr_fp64", 1);   // no task block: MuJoCo's fp64
   if (h->NV != 30 && h->NV != 33 && h->NV != 36) { delete h; return fail(AW_EUNSUPPORTED, "nv not instantiated"); }
   HIPCHK(hipSetDevice(device));
   HIPCHK(hipMalloc(&h->dmodel, sizeof(MData)));
@@ -994,7 +1006,7 @@ int aw_set_option(aw_handle* h, int disableflags, int iterations, int noslip_ite
 int aw_reset(aw_handle* h, const uint8_t* mask, const float* params, uint64_t seed, float* obs, void* stream) {
   if (!h) return fail(AW_EINVAL, "aw_reset: null");
   HIPCHK(hipSetDevice(h->device));
-#define CALL(NVV) launch_reset<NVV>(h, mask, params, seed, obs, (hipStream_t)stream)
+#define CALL(NVV) (mpr_kernel_fp64(h) ? launch_reset<NVV, 1>(h, mask, params, seed, obs, (hipStream_t)stream) : launch_reset<NVV, 0>(h, mask, params, seed, obs, (hipStream_t)stream))
   DISPATCH_NV(h->NV, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());
@@ -1005,7 +1017,7 @@ int aw_step(aw_handle* h, const float* actions, float* obs, float* reward, uint8
             float* terminal_obs, int autoreset, uint64_t seed, void* stream) {
   if (!h || !actions || !obs || !reward || !done || !goal) return fail(AW_EINVAL, "aw_step: null buffer");
   HIPCHK(hipSetDevice(h->device));
-#define CALL(NVV) launch_step<NVV>(h, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, (hipStream_t)stream)
+#define CALL(NVV) (mpr_kernel_fp64(h) ? launch_step<NVV, 1>(h, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, (hipStream_t)stream) : launch_step<NVV, 0>(h, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, (hipStream_t)stream))
   DISPATCH_NV(h->NV, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());
@@ -1038,7 +1050,7 @@ int aw_set_state(aw_handle* h, const float* qpos, const float* qvel, const float
                  float* obs, void* stream) {
   if (!h) return fail(AW_EINVAL, "aw_set_state: null");
   HIPCHK(hipSetDevice(h->device));
-#define CALL(NVV) launch_set<NVV>(h, qpos, qvel, warm, params, obs, (hipStream_t)stream)
+#define CALL(NVV) (mpr_kernel_fp64(h) ? launch_set<NVV, 1>(h, qpos, qvel, warm, params, obs, (hipStream_t)stream) : launch_set<NVV, 0>(h, qpos, qvel, warm, params, obs, (hipStream_t)stream))
   DISPATCH_NV(h->NV, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());
@@ -1079,7 +1091,7 @@ int aw_task_eval(aw_handle* h, int n, const float* qpos, const float* qvel, cons
 int aw_forward_dump(aw_handle* h, int env, const float* ctrl, float* out, void* stream) {
   if (!h || !out || env < 0 || env >= h->nenv) return fail(AW_EINVAL, "aw_forward_dump: bad arguments");
   HIPCHK(hipSetDevice(h->device));
-#define CALL(NVV) launch_dump<NVV>(h, env, ctrl, out, (hipStream_t)stream)
+#define CALL(NVV) (mpr_kernel_fp64(h) ? launch_dump<NVV, 1>(h, env, ctrl, out, (hipStream_t)stream) : launch_dump<NVV, 0>(h, env, ctrl, out, (hipStream_t)stream))
   DISPATCH_NV(h->NV, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());

@@ -448,88 +448,85 @@ AW_DEV void c_box_box(const GV& A, const GV& B, float margin, Emit& e) {
 // ---------------------------------------------------------------------------------------
 // MPR (libccd ccdMPRPenetration), supports inflated by margin/2 (mjccd_support)
 namespace mpr {
-// Precision: fp32 by default (libccd's float build, CCD_EPS = FLT_EPSILON).  -DAW_MPR_FP64 runs
-// MPR in fp64 like MuJoCo's double libccd (CCD_EPS = DBL_EPSILON): that removes the rare fp32
-// failures on shallow face-on-face contacts (a cylinder lying on a box: the portal can settle on
-// a side face) -- tests/test_gpu_parity.py::test_hammer_variations_one_step -- at ~9 % of
-// k_step time (MI355X fp64 VALU at half the fp32 rate, twice the registers).
-#ifdef AW_MPR_FP64
-using real = double;
-constexpr real EPS = 2.220446049250313e-16;  // DBL_EPSILON
-#else
-using real = float;
-constexpr real EPS = 1.1920928955078125e-07f;  // FLT_EPSILON
-#endif
-struct GVd {
-  real pos[3], mat[9], size[3];
+// Precision (template parameter T, from the kernels' MP parameter): fp64 like MuJoCo's double
+// libccd, or fp32 like libccd's float build -- per task (tasks.py TaskSpec.mpr_fp64),
+// overridable with aw_set_option.  fp32 mis-resolves shallow face-on-face contacts (a cylinder
+// lying on a box face, cm-scale portals whose squared sizes fall under FLT_EPSILON): pen-v0
+// teacher-forced parity 81 % in fp32, 99.9 % in fp64; hammer is as close in fp32 (99.8 %),
+// where fp64 would cost ~5 % of k_step time (fp64 VALU at half the fp32 rate, twice the
+// registers).
+// libccd's CCD_EPS of the matching build: DBL_EPSILON (MuJoCo's double build) / FLT_EPSILON
+template <class T> constexpr T EPS_T = sizeof(T) == 8 ? T(2.220446049250313e-16) : T(1.1920928955078125e-07);
+template <class T> struct GVdT {
+  T pos[3], mat[9], size[3];
   int type;
 };
-AW_DEV bool is_zero(real x) { return fabs(x) < EPS; }
-AW_DEV bool eq(real a, real b) {
-  real ab = fabs(a - b);
-  if (ab < EPS) return true;
-  real fa = fabs(a), fb = fabs(b);
-  return fb > fa ? ab < EPS * fb : ab < EPS * fa;
+template <class T> AW_DEV bool is_zero(T x) { return fabs(x) < EPS_T<T>; }
+template <class T> AW_DEV bool eq(T a, T b) {
+  T ab = fabs(a - b);
+  if (ab < EPS_T<T>) return true;
+  T fa = fabs(a), fb = fabs(b);
+  return fb > fa ? ab < EPS_T<T> * fb : ab < EPS_T<T> * fa;
 }
-AW_DEV bool veq(const real* a, const real* b) { return eq(a[0], b[0]) && eq(a[1], b[1]) && eq(a[2], b[2]); }
-AW_DEV void vnorm(real* v) {
-  real k = real(1.0) / sqrt(dot3(v, v));
+template <class T> AW_DEV bool veq(const T* a, const T* b) { return eq(a[0], b[0]) && eq(a[1], b[1]) && eq(a[2], b[2]); }
+template <class T> AW_DEV void vnorm(T* v) {
+  T k = T(1.0) / sqrt(dot3(v, v));
   scl3(v, v, k);
 }
-AW_DEV real sgn(real x) { return x < 0 ? -real(1.0) : (x > 0 ? real(1.0) : real(0.0)); }
+template <class T> AW_DEV T sgn(T x) { return x < 0 ? -T(1.0) : (x > 0 ? T(1.0) : T(0.0)); }
 
-struct Sup { real v[3], v1[3], v2[3]; };
+template <class T> struct SupT { T v[3], v1[3], v2[3]; };
 
 // support point of a primitive in direction dir (world), inflated by margin / 2.  Branch-free:
 // the lanes of one MPR round hold pairs of different geom types, and a type switch would run
 // every shape's branch in turn.
-AW_DEV void gsupport(real* res, const GVd& g, const real* dir, real margin) {
-  real ld[3], r[3];
+template <class T> AW_DEV void gsupport(T* res, const GVdT<T>& g, const T* dir, T margin) {
+  T ld[3], r[3];
   mulmtv3(ld, g.mat, dir);
-  const real* s = g.size;
+  const T* s = g.size;
   const bool box = g.type == GEOM_BOX, cyl = g.type == GEOM_CYLINDER, cap = g.type == GEOM_CAPSULE;
   const bool round = g.type == GEOM_SPHERE || cap;
-  const real sg0 = sgn(ld[0]), sg1 = sgn(ld[1]), sg2 = sgn(ld[2]);
-  const real tmp = sqrt(ld[0] * ld[0] + ld[1] * ld[1]);
-  const real ci = tmp > MINVAL ? s[0] / tmp : real(0.0);
-  r[0] = box ? sg0 * s[0] : (cyl ? ld[0] * ci : (round ? ld[0] * s[0] : real(0.0)));
-  r[1] = box ? sg1 * s[1] : (cyl ? ld[1] * ci : (round ? ld[1] * s[0] : real(0.0)));
-  r[2] = box ? sg2 * s[2] : (cyl ? sg2 * s[1] : (round ? fma(ld[2], s[0], cap ? sg2 * s[1] : real(0.0)) : real(0.0)));
+  const T sg0 = sgn(ld[0]), sg1 = sgn(ld[1]), sg2 = sgn(ld[2]);
+  const T tmp = sqrt(ld[0] * ld[0] + ld[1] * ld[1]);
+  const T ci = tmp > MINVAL ? s[0] / tmp : T(0.0);
+  r[0] = box ? sg0 * s[0] : (cyl ? ld[0] * ci : (round ? ld[0] * s[0] : T(0.0)));
+  r[1] = box ? sg1 * s[1] : (cyl ? ld[1] * ci : (round ? ld[1] * s[0] : T(0.0)));
+  r[2] = box ? sg2 * s[2] : (cyl ? sg2 * s[1] : (round ? fma(ld[2], s[0], cap ? sg2 * s[1] : T(0.0)) : T(0.0)));
   for (int k = 0; k < 3; k++) r[k] += ld[k] * margin / 2;
   mulmv3(res, g.mat, r);
   add3(res, res, g.pos);
 }
 
-struct Ctx { const GVd* g1; const GVd* g2; real margin, tol; int maxit; };
+template <class T> struct Ctx { const GVdT<T>* g1; const GVdT<T>* g2; T margin, tol; int maxit; };
 
-AW_DEV void support(const Ctx& c, const real* dir, Sup& s) {
-  real nd[3];
+template <class T> AW_DEV void support(const Ctx<T>& c, const T* dir, SupT<T>& s) {
+  T nd[3];
   scl3(nd, dir, -1);
   gsupport(s.v1, *c.g1, dir, c.margin);
   gsupport(s.v2, *c.g2, nd, c.margin);
   sub3(s.v, s.v1, s.v2);
 }
 // the portal is kept as four named vertices (no array) so every vertex stays in VGPRs
-struct Portal { Sup p0, p1, p2, p3; };
+template <class T> struct PortalT { SupT<T> p0, p1, p2, p3; };
 // element-wise copy (a whole-struct copy becomes a memcpy that keeps the portal in scratch)
-AW_DEV void setsup(Sup& d, const Sup& s) {
+template <class T> AW_DEV void setsup(SupT<T>& d, const SupT<T>& s) {
 #pragma unroll
   for (int k = 0; k < 3; k++) { d.v[k] = s.v[k]; d.v1[k] = s.v1[k]; d.v2[k] = s.v2[k]; }
 }
 
-AW_DEV void portal_dir(const Portal& P, real* dir) {
-  real a[3], b[3];
+template <class T> AW_DEV void portal_dir(const PortalT<T>& P, T* dir) {
+  T a[3], b[3];
   sub3(a, P.p2.v, P.p1.v);
   sub3(b, P.p3.v, P.p1.v);
   cross3(dir, a, b);
   vnorm(dir);
 }
-AW_DEV bool reach_tol(const Portal& P, const Sup& v4, const real* dir, real tol) {
-  real dv1 = dot3(P.p1.v, dir), dv2 = dot3(P.p2.v, dir), dv3 = dot3(P.p3.v, dir), dv4 = dot3(v4.v, dir);
-  real d1 = fmin(fmin(dv4 - dv1, dv4 - dv2), dv4 - dv3);
+template <class T> AW_DEV bool reach_tol(const PortalT<T>& P, const SupT<T>& v4, const T* dir, T tol) {
+  T dv1 = dot3(P.p1.v, dir), dv2 = dot3(P.p2.v, dir), dv3 = dot3(P.p3.v, dir), dv4 = dot3(v4.v, dir);
+  T d1 = fmin(fmin(dv4 - dv1, dv4 - dv2), dv4 - dv3);
   return eq(d1, tol) || d1 < tol;
 }
-AW_DEV void selsup(Sup& d, bool c, const Sup& s) {
+template <class T> AW_DEV void selsup(SupT<T>& d, bool c, const SupT<T>& s) {
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     d.v[k] = c ? s.v[k] : d.v[k]; d.v1[k] = c ? s.v1[k] : d.v1[k]; d.v2[k] = c ? s.v2[k] : d.v2[k];
@@ -537,8 +534,8 @@ AW_DEV void selsup(Sup& d, bool c, const Sup& s) {
 }
 // branch-free vertex replacement: conditional struct stores through a selected pointer would
 // pin the portal in scratch
-AW_DEV void expand(Portal& P, const Sup& v4) {
-  real v4v0[3];
+template <class T> AW_DEV void expand(PortalT<T>& P, const SupT<T>& v4) {
+  T v4v0[3];
   cross3(v4v0, v4.v, P.p0.v);
   const bool a1 = dot3(P.p1.v, v4v0) > 0;
   const bool a2 = dot3(P.p2.v, v4v0) > 0;
@@ -547,17 +544,17 @@ AW_DEV void expand(Portal& P, const Sup& v4) {
   selsup(P.p3, a1 && !a2, v4);
   selsup(P.p2, !a1 && a3, v4);
 }
-AW_DEV int discover(const Ctx& c, Portal& P) {
-  real dir[3], va[3], vb[3];
+template <class T> AW_DEV int discover(const Ctx<T>& c, PortalT<T>& P) {
+  T dir[3], va[3], vb[3];
   copy3(P.p0.v1, c.g1->pos);
   copy3(P.p0.v2, c.g2->pos);
   sub3(P.p0.v, P.p0.v1, P.p0.v2);
-  const real zero[3] = {0, 0, 0};
-  if (veq(P.p0.v, zero)) P.p0.v[0] += EPS * 10;
+  const T zero[3] = {0, 0, 0};
+  if (veq(P.p0.v, zero)) P.p0.v[0] += EPS_T<T> * 10;
   scl3(dir, P.p0.v, -1);
   vnorm(dir);
   support(c, dir, P.p1);
-  real d = dot3(P.p1.v, dir);
+  T d = dot3(P.p1.v, dir);
   if (is_zero(d) || d < 0) return -1;
   cross3(dir, P.p0.v, P.p1.v);
   if (is_zero(dot3(dir, dir))) return veq(P.p1.v, zero) ? 1 : 2;
@@ -571,7 +568,7 @@ AW_DEV int discover(const Ctx& c, Portal& P) {
   vnorm(dir);
   {
     const bool sw = dot3(dir, P.p0.v) > 0;
-    Sup t;
+    SupT<T> t;
     setsup(t, P.p1);
     selsup(P.p1, sw, P.p2);
     selsup(P.p2, sw, t);
@@ -597,27 +594,27 @@ AW_DEV int discover(const Ctx& c, Portal& P) {
   }
   return -1;
 }
-AW_DEV int refine(const Ctx& c, Portal& P) {
-  real dir[3];
-  Sup v4;
+template <class T> AW_DEV int refine(const Ctx<T>& c, PortalT<T>& P) {
+  T dir[3];
+  SupT<T> v4;
   for (int it = 0; it <= c.maxit; it++) {
     portal_dir(P, dir);
-    real d = dot3(dir, P.p1.v);
+    T d = dot3(dir, P.p1.v);
     if (is_zero(d) || d > 0) return 0;
     support(c, dir, v4);
-    real d4 = dot3(v4.v, dir);
+    T d4 = dot3(v4.v, dir);
     if (!(is_zero(d4) || d4 > 0) || reach_tol(P, v4, dir, c.tol)) return -1;
     expand(P, v4);
   }
   return -1;
 }
-AW_DEV real pseg2(const real* P, const real* x0, const real* b, real* w) {
-  real dd[3], a[3];
+template <class T> AW_DEV T pseg2(const T* P, const T* x0, const T* b, T* w) {
+  T dd[3], a[3];
   sub3(dd, b, x0);
   sub3(a, x0, P);
-  real t = -dot3(a, dd) / dot3(dd, dd);
-  const bool lo = t < 0 || is_zero(t), hi = !lo && (t > 1 || eq(t, 1));
-  real df[3];
+  T t = -dot3(a, dd) / dot3(dd, dd);
+  const bool lo = t < 0 || is_zero(t), hi = !lo && (t > 1 || eq(t, T(1)));
+  T df[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     w[k] = lo ? x0[k] : (hi ? b[k] : x0[k] + dd[k] * t);
@@ -625,25 +622,25 @@ AW_DEV real pseg2(const real* P, const real* x0, const real* b, real* w) {
   }
   return dot3(df, df);
 }
-AW_DEV real ptri2(const real* P, const real* x0, const real* B, const real* C, real* w) {
-  real d1[3], d2[3], a[3];
+template <class T> AW_DEV T ptri2(const T* P, const T* x0, const T* B, const T* C, T* w) {
+  T d1[3], d2[3], a[3];
   sub3(d1, B, x0);
   sub3(d2, C, x0);
   sub3(a, x0, P);
-  real v = dot3(d1, d1), ww = dot3(d2, d2), p = dot3(a, d1), q = dot3(a, d2), r = dot3(d1, d2);
-  real dd = ww * v - r * r, s, t;
+  T v = dot3(d1, d1), ww = dot3(d2, d2), p = dot3(a, d1), q = dot3(a, d2), r = dot3(d1, d2);
+  T dd = ww * v - r * r, s, t;
   if (is_zero(dd)) { s = t = -1; }
   else { s = (q * r - ww * p) / dd; t = (-s * r - q) / ww; }
-  if ((is_zero(s) || s > 0) && (eq(s, 1) || s < 1) && (is_zero(t) || t > 0) && (eq(t, 1) || t < 1) &&
-      (eq(t + s, 1) || t + s < 1)) {
+  if ((is_zero(s) || s > 0) && (eq(s, T(1)) || s < 1) && (is_zero(t) || t > 0) && (eq(t, T(1)) || t < 1) &&
+      (eq(t + s, T(1)) || t + s < 1)) {
     for (int k = 0; k < 3; k++) w[k] = x0[k] + d1[k] * s + d2[k] * t;
-    real df[3];
+    T df[3];
     sub3(df, w, P);
     return dot3(df, df);
   }
-  real w2[3];
-  real dist = pseg2(P, x0, B, w);
-  real d2s = pseg2(P, x0, C, w2);
+  T w2[3];
+  T dist = pseg2(P, x0, B, w);
+  T d2s = pseg2(P, x0, C, w2);
   bool take = d2s < dist;
   dist = take ? d2s : dist;
 #pragma unroll
@@ -655,14 +652,14 @@ AW_DEV real ptri2(const real* P, const real* x0, const real* B, const real* C, r
   for (int k = 0; k < 3; k++) w[k] = take ? w2[k] : w[k];
   return dist;
 }
-AW_DEV void find_pos(const Portal& P, real* pos) {
-  real dir[3], vec[3], b0, b1, b2, b3;
+template <class T> AW_DEV void find_pos(const PortalT<T>& P, T* pos) {
+  T dir[3], vec[3], b0, b1, b2, b3;
   portal_dir(P, dir);
   cross3(vec, P.p1.v, P.p2.v); b0 = dot3(vec, P.p3.v);
   cross3(vec, P.p3.v, P.p2.v); b1 = dot3(vec, P.p0.v);
   cross3(vec, P.p0.v, P.p1.v); b2 = dot3(vec, P.p3.v);
   cross3(vec, P.p2.v, P.p1.v); b3 = dot3(vec, P.p0.v);
-  real sum = b0 + b1 + b2 + b3;
+  T sum = b0 + b1 + b2 + b3;
   if (is_zero(sum) || sum < 0) {
     b0 = 0;
     cross3(vec, P.p2.v, P.p3.v); b1 = dot3(vec, dir);
@@ -670,39 +667,39 @@ AW_DEV void find_pos(const Portal& P, real* pos) {
     cross3(vec, P.p1.v, P.p2.v); b3 = dot3(vec, dir);
     sum = b1 + b2 + b3;
   }
-  real inv = real(1.0) / sum;
+  T inv = T(1.0) / sum;
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    real p1 = P.p0.v1[k] * b0 + P.p1.v1[k] * b1 + P.p2.v1[k] * b2 + P.p3.v1[k] * b3;
-    real p2 = P.p0.v2[k] * b0 + P.p1.v2[k] * b1 + P.p2.v2[k] * b2 + P.p3.v2[k] * b3;
-    pos[k] = real(0.5) * (p1 + p2) * inv;
+    T p1 = P.p0.v1[k] * b0 + P.p1.v1[k] * b1 + P.p2.v1[k] * b2 + P.p3.v1[k] * b3;
+    T p2 = P.p0.v2[k] * b0 + P.p1.v2[k] * b1 + P.p2.v2[k] * b2 + P.p3.v2[k] * b3;
+    pos[k] = T(0.5) * (p1 + p2) * inv;
   }
 }
-AW_DEV int penetration(const Ctx& c, real* depth, real* dir, real* pos) {
-  Portal P;
+template <class T> AW_DEV int penetration(const Ctx<T>& c, T* depth, T* dir, T* pos) {
+  PortalT<T> P;
   int res = discover(c, P);
   if (res < 0) return -1;
   if (res == 1) {
     *depth = 0;
     dir[0] = dir[1] = dir[2] = 0;
-    for (int k = 0; k < 3; k++) pos[k] = real(0.5) * (P.p1.v1[k] + P.p1.v2[k]);
+    for (int k = 0; k < 3; k++) pos[k] = T(0.5) * (P.p1.v1[k] + P.p1.v2[k]);
     return 0;
   }
   if (res == 2) {
-    for (int k = 0; k < 3; k++) pos[k] = real(0.5) * (P.p1.v1[k] + P.p1.v2[k]);
+    for (int k = 0; k < 3; k++) pos[k] = T(0.5) * (P.p1.v1[k] + P.p1.v2[k]);
     copy3(dir, P.p1.v);
     *depth = sqrt(dot3(dir, dir));
     vnorm(dir);
     return 0;
   }
   if (refine(c, P) < 0) return -1;
-  Sup v4;
-  real pd[3];
+  SupT<T> v4;
+  T pd[3];
   for (int it = 0;; it++) {
     portal_dir(P, pd);
     support(c, pd, v4);
     if (reach_tol(P, v4, pd, c.tol) || it > c.maxit) {
-      const real zero[3] = {0, 0, 0};
+      const T zero[3] = {0, 0, 0};
       *depth = sqrt(ptri2(zero, P.p1.v, P.p2.v, P.p3.v, dir));
       if (is_zero(*depth)) dir[0] = dir[1] = dir[2] = 0;
       else vnorm(dir);
@@ -714,13 +711,16 @@ AW_DEV int penetration(const Ctx& c, real* depth, real* dir, real* pos) {
 }
 }  // namespace mpr
 
+template <class T>
 AW_DEV void c_convex(const DModel& m, const GV& a, const GV& b, float margin, Emit& e) {
-  mpr::GVd ad, bd;
-  for (int k = 0; k < 3; k++) { ad.pos[k] = a.pos[k]; ad.size[k] = a.size[k]; bd.pos[k] = b.pos[k]; bd.size[k] = b.size[k]; }
+  mpr::GVdT<T> ad, bd;
+  for (int k = 0; k < 3; k++) {
+    ad.pos[k] = a.pos[k]; ad.size[k] = a.size[k]; bd.pos[k] = b.pos[k]; bd.size[k] = b.size[k];
+  }
   for (int k = 0; k < 9; k++) { ad.mat[k] = a.mat[k]; bd.mat[k] = b.mat[k]; }
   ad.type = a.type; bd.type = b.type;
-  mpr::Ctx ctx{&ad, &bd, (mpr::real)margin, (mpr::real)m.mpr_tolerance, m.mpr_iterations};
-  mpr::real depth, dir[3], pos[3];
+  mpr::Ctx<T> ctx{&ad, &bd, (T)margin, (T)m.mpr_tolerance, m.mpr_iterations};
+  T depth, dir[3], pos[3];
   if (mpr::penetration(ctx, &depth, dir, pos) != 0) return;
   if (dir[0] == 0 && dir[1] == 0 && dir[2] == 0) return;
   const float dist = margin - (float)depth;
@@ -735,7 +735,7 @@ AW_DEV void c_convex(const DModel& m, const GV& a, const GV& b, float margin, Em
 // 0 plane-*, 1 sphere/capsule pairs, 2 sphere/capsule-box, 3 box-box, 4 anything with a
 // cylinder (MPR).  The class is a template parameter so each class loop carries only its own
 // colliders (no divergent merge of every collider's code and registers).
-template <int C>
+template <int C, int MP>
 AW_DEV void collide_pair(const DModel& m, Env& s, int pair) {
   int g1 = MD(cp_g1, pair), g2 = MD(cp_g2, pair);
   GV a, b;
@@ -754,7 +754,8 @@ AW_DEV void collide_pair(const DModel& m, Env& s, int pair) {
   }
   Emit e{&s, pair, 0};
   if constexpr (C == 4) {           // every non-plane pair with a cylinder: MPR (mjc_Convex)
-    c_convex(m, a, b, margin, e);
+    if constexpr (MP) c_convex<double>(m, a, b, margin, e);
+    else c_convex<float>(m, a, b, margin, e);
   } else if constexpr (C == 0) {
     if (b.type == GEOM_SPHERE) c_plane_sphere(a.pos, a.mat, b.pos, b.size[0], margin, e);
     else if (b.type == GEOM_CAPSULE) c_plane_capsule(a, b, margin, e);

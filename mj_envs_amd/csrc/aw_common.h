@@ -80,6 +80,8 @@ enum {
   DSBL_PASSIVE = 1 << 5, DSBL_GRAVITY = 1 << 6, DSBL_CLAMPCTRL = 1 << 7, DSBL_WARMSTART = 1 << 8,
   DSBL_ACTUATION = 1 << 10, DSBL_REFSAFE = 1 << 11, DSBL_SENSOR = 1 << 12, DSBL_NOSLIP = 1 << 14,
   DSBL_EULERDAMP = 1 << 15,
+  DSBL_MPR_FP64 = 1 << 16,   // ours: run the MPR (cylinder) collider in fp32
+  DSBL_MPR_FP32 = 1 << 17,   // ours: run it in fp64 (neither bit: the task's default)
 };
 enum { ST_BADQPOS = 1, ST_BADQVEL = 2, ST_BADQACC = 4, ST_CON_OVERFLOW = 8, ST_EFC_OVERFLOW = 16 };
 

@@ -244,11 +244,28 @@ def test_determinism():
 # exit then lands one sweep apart from the fp64 oracle's (6 vs 5 sweeps: ~1 % qacc change in that
 # substep).  tools/debug_sub.py shows forward internals identical to 4e-7 relative up to that
 # substep.
-TEACHER_FORCED_MIN = {"hammer-v0": 0.95, "door-v0": 0.95, "relocate-v0": 0.95, "pen-v0": 0.75}
+TEACHER_FORCED_MIN = {"hammer-v0": 0.97, "door-v0": 0.97, "relocate-v0": 0.97, "pen-v0": 0.97}
+# the MPR collider forced to the other precision than the task default (tasks.py mpr_fp64):
+# pen in fp32 resolves shallow face-on-face cylinder contacts differently (~81 %, see
+# aw_collide.h namespace mpr); hammer / door in fp64
+TEACHER_FORCED_MIN_MPR_OTHER = {"hammer-v0": 0.97, "door-v0": 0.97, "pen-v0": 0.75}
 
 
 @pytest.mark.parametrize("env_id", ENVS)
 def test_teacher_forced_trajectory(env_id):
+    frac = _teacher_forced(env_id, 0)
+    assert frac >= TEACHER_FORCED_MIN[env_id], (env_id, frac)
+
+
+@pytest.mark.parametrize("env_id", sorted(TEACHER_FORCED_MIN_MPR_OTHER))
+def test_teacher_forced_trajectory_other_mpr_precision(env_id):
+    from mj_envs_amd._native import DSBL_MPR_FP32, DSBL_MPR_FP64
+    from mj_envs_amd.tasks import TASKS
+    frac = _teacher_forced(env_id, DSBL_MPR_FP64 if TASKS[env_id].mpr_fp64 else DSBL_MPR_FP32)
+    assert frac >= TEACHER_FORCED_MIN_MPR_OTHER[env_id], (env_id, frac)
+
+
+def _teacher_forced(env_id, disableflags):
     """SURVEY §8d C3 (multi-task correctness vs the CPU path): along a 40-step GPU rollout of
     64 envs, every env-step is re-run by the fp64 oracle from the GPU's own pre-step state
     (qpos, qvel, warmstart, params) with the same action; the GPU's post-step state must match
@@ -260,6 +277,7 @@ def test_teacher_forced_trajectory(env_id):
     m, o = make_oracle(env_id)
     o.set_option(max_con=32, max_efc=128)
     _, sim = _sim(env_id, n)
+    sim.set_option(disableflags=disableflags)
     P = sample_params(env_id, m, np.random.default_rng(11), n)
     obs = sim.empty(n, sim.obs_dim)
     sim.reset(obs, params=_t(P))
@@ -286,9 +304,10 @@ def test_teacher_forced_trajectory(env_id):
         rg = rew.cpu().numpy()
         rok.append(np.abs(rg - r_ref)[ok] <= 1e-3 + 1e-3 * np.abs(r_ref[ok]))
     frac = np.concatenate(oks).mean()
-    print(f"teacher-forced {env_id}: {frac:.4f} of (env, step) cases within tolerance")
-    assert frac >= TEACHER_FORCED_MIN[env_id], (env_id, frac)
+    print(f"teacher-forced {env_id} (disableflags {disableflags:#x}): {frac:.4f} of (env, step) cases "
+          f"within tolerance")
     assert np.concatenate(rok).all(), env_id
+    return frac
 
 
 @pytest.mark.parametrize("variation", ["mass", "pos", "size"])
