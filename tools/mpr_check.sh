@@ -1,3 +1,4 @@
+# GPU suite + hammer (task default / forced fp64 MPR) + pen benches (run through gpurun)
 set -e -o pipefail
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -s --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 grep -E "teacher-forced|passed|failed" gpurun_out/pytest_gpu.log
