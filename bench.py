@@ -107,6 +107,9 @@ def main():
                     help="strong scaling: fixed total envs split over the ranks (e.g. 262144, SURVEY C4)")
     ap.add_argument("--env", default=ENV_ID)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-config2", action="store_true",
+                    help="skip the auxiliary 4 096-env figure (profiling runs: every k_step launch is then "
+                         "the headline size, so rocprof's average matches roofline.kernel_ms)")
     ap.add_argument("--policy", action="store_true",
                     help="closed loop: actions from the on-device Gaussian MLP (mjrl MLP, 32x32) instead of i.i.d.")
     ap.add_argument("--mpr", choices=("task", "fp32", "fp64"), default="task",
@@ -244,7 +247,8 @@ def main():
                     config=dict(workload=workload, envs_per_gpu=n, total_envs=world * n,
                                 frame_skip=sim.frame_skip, parallelism=f"env-shard x{world}"),
                     roofline=roof, finite=finite)
-        if world == 1 and env_id == ENV_ID and depth is None and pol is None and n == 65536 and args.mpr == "task":
+        if world == 1 and env_id == ENV_ID and depth is None and pol is None and n == 65536 and args.mpr == "task" \
+                and not args.no_config2:
             line["config2_4096_envs"] = config2(blob, env_id, local)
         if world == 1 and not args.no_cpu_baseline:
             try:

@@ -16,9 +16,9 @@ echo "[gpu_round] bench"
 timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err
 cat $OUT/bench.json
 echo "[gpu_round] kernel trace"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o kt -- python bench.py --steps 30 --warmup 5 --no-cpu-baseline > $OUT/trace.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o kt -- python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-config2 > $OUT/trace.log 2>&1
 echo "[gpu_round] pmc fetch"
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pf -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/pmc_fetch.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pf -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-config2 > $OUT/pmc_fetch.log 2>&1
 echo "[gpu_round] pmc write"
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o pw -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/pmc_write.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o pw -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-config2 > $OUT/pmc_write.log 2>&1
 echo "[gpu_round] done"
