@@ -315,9 +315,25 @@ AW_DEV void reset_env(const DModel& m, Env& s, const DState& st, int env, int la
 // substeps, the mj_checkAcc retry and the reset forward through it), which keeps the code
 // object small enough for the instruction cache.
 template <int NV, int MP>
-__global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel m, DState st, int n, const float* __restrict__ actions,
+__global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DModel* __restrict__ mptr, DState stval,
+                                             int n, const float* __restrict__ actions,
                                              float* obs, float* reward, uint8_t* done, uint8_t* goal,
                                              float* terminal_obs, int autoreset, uint64_t seed) {
+#ifndef AW_MODEL_BYVAL
+  // model scalars read from the device copy on demand (scalar loads behind the loop's memory
+  // clobber) instead of ~50 kernel-argument SGPRs held live across the whole launch
+  const DModel& m = *mptr;
+  (void)mval;
+#else
+  const DModel& m = mval;
+  (void)mptr;
+#endif
+#ifdef AW_STATE_PTR
+  const DState& st = *reinterpret_cast<const DState*>(mptr + 1);   // DState follows DModel in the header
+  (void)stval;
+#else
+  const DState& st = stval;
+#endif
   __shared__ Env s;
   const int env = blockIdx.x, lane = threadIdx.x;
   if (env >= n) return;
@@ -591,8 +607,15 @@ struct aw_handle {
   DModel m;
   DState st;
   void* dmodel = nullptr;
+  void* dmhdr = nullptr;   // device copy of m (k_step reads its scalars from here)
   void* dstate = nullptr;
 };
+
+static int upload_header(aw_handle* h) {
+  HIPCHK(hipMemcpy(h->dmhdr, &h->m, sizeof(DModel), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy((DModel*)h->dmhdr + 1, &h->st, sizeof(DState), hipMemcpyHostToDevice));
+  return AW_OK;
+}
 
 static int build_model(const Blob& B, DModel& m, MData& md) {
   memset(&m, 0, sizeof(m));
@@ -877,7 +900,7 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
 template <int NV, int MP>
 static void launch_step(aw_handle* h, const float* a, float* obs, float* rew, uint8_t* done, uint8_t* goal,
                         float* tobs, int autoreset, uint64_t seed, hipStream_t st) {
-  hipLaunchKernelGGL((k_step<NV, MP>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, a, obs, rew, done,
+  hipLaunchKernelGGL((k_step<NV, MP>), dim3(h->nenv), dim3(64), 0, st, h->m, (const DModel*)h->dmhdr, h->st, h->nenv, a, obs, rew, done,
                      goal, tobs, autoreset, seed);
 }
 template <int NV, int MP>
@@ -944,6 +967,7 @@ int aw_create(const void* blob, size_t nbytes, int n_envs, int device, aw_handle
   HIPCHK(hipMalloc(&h->dmodel, sizeof(MData)));
   HIPCHK(hipMemcpy(h->dmodel, md.get(), sizeof(MData), hipMemcpyHostToDevice));
   h->m.d = (const MData*)h->dmodel;
+  HIPCHK(hipMalloc(&h->dmhdr, sizeof(DModel) + sizeof(DState)));
   // state
   size_t N = (size_t)n_envs, nq = h->m.nq, nv = h->m.nv, np = std::max(h->m.nparam, 1);
   size_t bytes = N * (nq + 2 * nv + np) * 4 + N * 4 * 10 + 256;
@@ -973,6 +997,7 @@ int aw_create(const void* blob, size_t nbytes, int n_envs, int device, aw_handle
   for (size_t e = 0; e < N; e++)
     for (int k = 0; k < h->m.nparam; k++) prm[e * np + k] = (float)def[k];
   HIPCHK(hipMemcpy(h->st.params, prm.data(), prm.size() * 4, hipMemcpyHostToDevice));
+  if (int rc2 = upload_header(h)) return rc2;
   *out = h;
   return AW_OK;
 }
@@ -981,6 +1006,7 @@ int aw_destroy(aw_handle* h) {
   if (!h) return AW_OK;
   hipSetDevice(h->device);
   if (h->dmodel) hipFree(h->dmodel);
+  if (h->dmhdr) hipFree(h->dmhdr);
   if (h->dstate) hipFree(h->dstate);
   delete h;
   return AW_OK;
@@ -1000,7 +1026,8 @@ int aw_set_option(aw_handle* h, int disableflags, int iterations, int noslip_ite
   if (disableflags >= 0) h->m.disableflags = disableflags;
   if (iterations >= 0) h->m.iterations = iterations;
   if (noslip_iterations >= 0) h->m.noslip_iterations = noslip_iterations;
-  return AW_OK;
+  HIPCHK(hipSetDevice(h->device));
+  return upload_header(h);
 }
 
 int aw_reset(aw_handle* h, const uint8_t* mask, const float* params, uint64_t seed, float* obs, void* stream) {
