@@ -69,7 +69,8 @@ int aw_dims(const aw_handle* h, int* dims /* [AW_NDIMS] */);
 /* MuJoCo-style disable flags (mjtDisableBit values; bit 14 = noslip, bit 15 = explicit
  * damping, bit 16 = MPR (cylinder) collider in fp32, bit 17 = MPR collider in fp64; neither:
  * the task's default from the model blob, task_mpr_fp64) and solver iteration counts;
- * negative values keep the current setting. */
+ * negative values keep the current setting.  Waits for the device (queued steps finish with
+ * the old options), then re-uploads the model header that k_step reads. */
 int aw_set_option(aw_handle* h, int disableflags, int iterations, int noslip_iterations);
 
 /* Reset envs (mask[e] != 0, or all if mask == NULL): qpos = qpos0, qvel = 0, warmstart = 0,

@@ -1027,6 +1027,7 @@ int aw_set_option(aw_handle* h, int disableflags, int iterations, int noslip_ite
   if (iterations >= 0) h->m.iterations = iterations;
   if (noslip_iterations >= 0) h->m.noslip_iterations = noslip_iterations;
   HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipDeviceSynchronize());   // steps already queued on any stream read the old header
   return upload_header(h);
 }
 
