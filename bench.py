@@ -4,17 +4,20 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-A "step" = one env-step of every env on every GPU: i.i.d. U(-1,1) actions from Philox
-(seed 0, counter (env, step)), 5 physics substeps (frame_skip) + reward + obs, auto-reset at
-the 200-step horizon inside the timed region, and at every episode boundary an RCCL all-gather
-of the per-env episode returns / goal counts over xGMI.  Weak scaling: envs per GPU fixed
-(default 65 536 = the north-star configuration).  Inputs are resident in HBM; value is
-whole-job env-steps/s = N * envs_per_gpu * K / max-over-ranks wall time.
+A "step" = one env-step of every env on every GPU: i.i.d. U(-1,1) actions from Philox (seed 0,
+counter (global env id, step)), frame_skip = 5 physics substeps + reward + obs, and auto-reset
+inside the kernel whenever an episode ends.  Episode phases are staggered (each env's first
+episode starts at a hash of its global id modulo the horizon) and an untimed pre-roll of one
+horizon runs before the warm-up, so every timed window is in steady state: ~N/200 envs end an
+episode and reset on every step, and all episode phases are present.  Every `horizon` steps
+(and at the end) the per-env totals over finished episodes (count, summed return, successes)
+are all-gathered over RCCL / xGMI -- every finished episode is counted once, whenever it
+ended.  Weak scaling: envs per GPU fixed (default 65 536 = the north-star configuration).
+Inputs are resident in HBM; value = N * envs_per_gpu * K / max-over-ranks wall time.
 """
 import argparse
 import json
 import os
-import subprocess
 import sys
 import time
 
@@ -22,41 +25,102 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 ENV_ID = "hammer-v0"
+SEED_RESET, SEED_ACT = 1, 0
 
 
-def cpu_baseline(model_blob, env_id, budget_s=12.0):
-    """Oracle (fp64 restatement, OpenMP over envs) on the host cores: bounded sample, all cores
-    (2/3 of the budget) and one core (1/3), BASELINE.md §2."""
+def cpu_threads():
+    """Host threads available to this job: the CPU affinity mask, capped by OMP_NUM_THREADS (the
+    GPU box grants 16 per GPU and sets it; nproc there reports the whole machine)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(omp)) if omp else aff), aff
+
+
+def gpu_inputs(blob, n, steps, local):
+    """The GPU run's own inputs for the first n envs: reset params (Philox, seed SEED_RESET,
+    global env ids 0..n-1) and `steps` steps of actions (seed SEED_ACT), copied to the host."""
     import numpy as np
-    from mj_envs_amd.tasks import attach_task, load_model, sample_params
+    import torch
+    from mj_envs_amd import _native
+    sim = _native.Sim(blob, n, device=local)
+    obs = sim.empty(n, sim.obs_dim)
+    sim.reset(obs, seed=SEED_RESET)
+    p = sim.empty(n, sim.nparam)
+    sim.get_state(params=p)
+    act = sim.empty(steps, n, sim.nu)
+    for k in range(steps):
+        sim.random_actions(act[k], SEED_ACT, k)
+    torch.cuda.synchronize()
+    out = p.cpu().numpy().astype(np.float64), act.cpu().numpy().astype(np.float64)
+    sim.close()
+    return out
+
+
+def cpu_baseline(blob, env_id, local, budget_s=12.0):
+    """Oracle (fp64 restatement, OpenMP over envs) on the host cores, on the GPU run's own reset
+    params and Philox actions: all available threads (2/3 of the budget) and one (1/3)."""
     from oracle.pyoracle import Oracle, build
     build()
-    m = attach_task(load_model(env_id), env_id)
-    o = Oracle(model_blob)
-    o.set_option(max_con=32, max_efc=128)
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    threads = max(1, min(threads, 16))
+    o = Oracle(blob)
+    threads, aff = cpu_threads()
 
     def run(nth, budget):
         n = 64 * nth
-        rng = np.random.default_rng(0)
-        P = sample_params(env_id, m, rng, n)
+        P, A = gpu_inputs(blob, n, 600, local)
         st, _ = o.reset(P, nthreads=nth)
         steps = 0
         t0 = time.perf_counter()
-        while time.perf_counter() - t0 < budget:
-            o.step(st, rng.uniform(-1, 1, (n, o.nu)), nthreads=nth)
+        while time.perf_counter() - t0 < budget and steps < A.shape[0]:
+            o.step(st, A[steps], nthreads=nth)
             steps += 1
         dt = time.perf_counter() - t0
         return n * steps / dt, n, steps, dt
 
     v, n, steps, dt = run(threads, budget_s * 2 / 3)
     v1, n1, steps1, dt1 = run(1, budget_s / 3)
-    return dict(value=v, unit="env-steps/s", cores=threads, kind="port",
-                single_core_value=v1,
-                sample=f"{env_id}, {n} envs x {steps} env-steps (random policy) on {threads} threads in {dt:.1f} s "
-                       f"and {n1} envs x {steps1} env-steps on 1 thread in {dt1:.1f} s; fp64 C++ oracle "
-                       f"(restated mj_step + task layer), OpenMP over envs")
+    return dict(value=round(v, 1), unit="env-steps/s", cores=threads, kind="port",
+                single_core_value=round(v1, 1), nproc=os.cpu_count(), affinity_cpus=aff,
+                omp_num_threads=os.environ.get("OMP_NUM_THREADS"),
+                sample=f"{env_id}, the GPU run's first {n} envs (its Philox reset params and actions) x {steps} "
+                       f"env-steps on {threads} threads in {dt:.1f} s, and {n1} envs x {steps1} env-steps on 1 "
+                       f"thread in {dt1:.1f} s; fp64 C++ oracle (restated mj_step + task layer at MuJoCo's "
+                       f"capacities), OpenMP over envs; threads = the job's CPU share (affinity / OMP_NUM_THREADS)")
+
+
+def same_run_parity(blob, env_id, sim, local, n=256):
+    """One env-step from the benchmark's own mid-run states (first n envs) on the GPU and on the
+    fp64 oracle: fraction within the one-step tolerance of tests/test_gpu_parity.py and errors."""
+    import numpy as np
+    import torch
+    from mj_envs_amd import _native
+    from oracle.pyoracle import Oracle, build
+    build()
+    q, v, w, p = (sim.empty(sim.n_envs, sim.nq), sim.empty(sim.n_envs, sim.nv), sim.empty(sim.n_envs, sim.nv),
+                  sim.empty(sim.n_envs, sim.nparam))
+    sim.get_state(q, v, w, p)
+    small = _native.Sim(blob, n, device=local)
+    small.set_state(q[:n].contiguous(), v[:n].contiguous(), w[:n].contiguous(), p[:n].contiguous())
+    act = small.empty(n, small.nu)
+    small.random_actions(act, 12345, 0)
+    obs, rew = small.empty(n, small.obs_dim), small.empty(n)
+    done, goal = small.empty(n, dtype=torch.uint8), small.empty(n, dtype=torch.uint8)
+    small.step(act, obs, rew, done, goal)
+    q2, v2 = small.empty(n, small.nq), small.empty(n, small.nv)
+    small.get_state(q2, v2)
+    torch.cuda.synchronize()
+    st = dict(qpos=q[:n].cpu().numpy().astype(np.float64), qvel=v[:n].cpu().numpy().astype(np.float64),
+              warm=w[:n].cpu().numpy().astype(np.float64), params=p[:n].cpu().numpy().astype(np.float64))
+    o = Oracle(blob)
+    o_obs, o_rew, _, _, _ = o.step(st, act.cpu().numpy().astype(np.float64))
+    qg, vg = q2.cpu().numpy(), v2.cpu().numpy()
+    okq = (np.abs(qg - st["qpos"]) <= 2e-5 + 1e-5 * np.abs(st["qpos"])).all(axis=1)
+    okv = (np.abs(vg - st["qvel"]) <= 5e-3 * (1 + np.abs(st["qvel"]))).all(axis=1)
+    small.close()
+    return dict(envs=n, frac_within_tol=round(float((okq & okv).mean()), 4),
+                max_abs_qpos=float(np.abs(qg - st["qpos"]).max()),
+                median_abs_obs=float(np.median(np.abs(obs.cpu().numpy() - o_obs))),
+                max_abs_reward=float(np.abs(rew.cpu().numpy() - o_rew).max()),
+                tolerance="qpos 2e-5 + 1e-5|q|, qvel 5e-3 (1 + |v|) per env (tests/test_gpu_parity.py)")
 
 
 def config2(blob, env_id, device, n=4096, steps=100, warmup=10):
@@ -81,20 +145,20 @@ def config2(blob, env_id, device, n=4096, steps=100, warmup=10):
 
 
 def pmc_traffic(env_per_launch):
-    """HBM bytes per k_step launch from the committed rocprofv3 --pmc summary, or None."""
+    """HBM bytes per k_step launch from the latest committed rocprofv3 --pmc summary, or None."""
     import glob
     paths = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_kstep.json")))
     if not paths:
-        return None
-    path = paths[-1]                         # latest round's counters
+        return None, None
+    path = paths[-1]
     try:
         with open(path) as f:
             d = json.load(f)
         if d.get("envs") != env_per_launch:
-            return None
-        return d.get("hbm_bytes_per_launch")
+            return None, None
+        return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO)
     except Exception:
-        return None
+        return None, None
 
 
 def main():
@@ -102,16 +166,21 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--preroll", type=int, default=-1,
+                    help="untimed steps after the staggered reset (default: one horizon), so the timed "
+                         "window starts in steady state")
     ap.add_argument("--envs-per-gpu", type=int, default=65536)
     ap.add_argument("--total-envs", type=int, default=0,
                     help="strong scaling: fixed total envs split over the ranks (e.g. 262144, SURVEY C4)")
     ap.add_argument("--env", default=ENV_ID)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-config2", action="store_true",
                     help="skip the auxiliary 4 096-env figure (profiling runs: every k_step launch is then "
                          "the headline size, so rocprof's average matches roofline.kernel_ms)")
-    ap.add_argument("--policy", action="store_true",
-                    help="closed loop: actions from the on-device Gaussian MLP (mjrl MLP, 32x32) instead of i.i.d.")
+    ap.add_argument("--policy", choices=("none", "random-mlp", "dapg"), default="none",
+                    help="closed loop: actions from the on-device Gaussian MLP (k_mlp): random init 32x32 "
+                         "(sampled), or the reference's pretrained DAPG policy (mean action)")
     ap.add_argument("--mpr", choices=("task", "fp32", "fp64"), default="task",
                     help="precision of the MPR (cylinder) collider: the task's default (tasks.py "
                          "TaskSpec.mpr_fp64; hammer fp32), or forced")
@@ -119,10 +188,11 @@ def main():
                     help="BASELINE config 5: + 64x64 depth-camera obs every env-step (default 8192 envs)")
     args = ap.parse_args()
 
+    import numpy as np
     import torch
     import torch.distributed as dist
     from mj_envs_amd import _native, perfmodel
-    from mj_envs_amd.dist import EpisodeGather, rank_seed, shard_from_env
+    from mj_envs_amd.dist import EpisodeTotals, shard_from_env, stagger_phases
     from mj_envs_amd.tasks import TASKS, attach_task, load_model
 
     if args.depth and args.envs_per_gpu == 65536:
@@ -144,7 +214,7 @@ def main():
     m = attach_task(load_model(env_id), env_id)
     blob = m.to_blob()
     n = args.envs_per_gpu
-    sim = _native.Sim(blob, n, device=local)
+    sim = _native.Sim(blob, n, device=local, env_offset=shard.env_offset)   # streams keyed by global id
     if args.mpr != "task":
         sim.set_option(disableflags=_native.DSBL_MPR_FP64 if args.mpr == "fp32" else _native.DSBL_MPR_FP32)
     mpr64 = args.mpr == "fp64" or (args.mpr == "task" and TASKS[env_id].mpr_fp64)
@@ -153,29 +223,40 @@ def main():
     rew = sim.empty(n)
     done = sim.empty(n, dtype=torch.uint8)
     goal = sim.empty(n, dtype=torch.uint8)
-    last_ret = sim.empty(n)
-    last_goal = sim.empty(n, dtype=torch.int32)
-    gather = EpisodeGather(n, world, dev)
-    seed = rank_seed(1, rank)                # per-rank Philox key: global env id = (rank, env)
-    sim.reset(obs, seed=seed)
+    tot_ep = sim.empty(n, dtype=torch.int32)
+    tot_ret = sim.empty(n)
+    tot_suc = sim.empty(n, dtype=torch.int32)
+    sticky = sim.empty(n, dtype=torch.int32)
+    totals = EpisodeTotals(n, world, dev)
+    sim.reset(obs, seed=SEED_RESET)
+    sim.set_episode(ep_len=torch.from_numpy(stagger_phases(n, shard.env_offset, sim.horizon)).to(dev))
     pol = None
-    if args.policy:
+    if args.policy == "random-mlp":
         from mj_envs_amd.policy import GaussianMLP
         pol = GaussianMLP(sim.obs_dim, sim.nu, (32, 32), init_log_std=-1.0, seed=0, device=local)
+    elif args.policy == "dapg":
+        from mj_envs_amd.policy import GaussianMLP
+        pol = GaussianMLP.from_npz(os.path.join(REPO, "tests", "golden", f"dapg_{env_id.split('-')[0]}.npz"),
+                                   device=local)
     depth = cam = None
     if args.depth:
         from mj_envs_amd.render import free_camera
         cam = free_camera(m, env_id, 64, 64)
         depth = sim.empty(n, 64, 64)
 
+    def gather():
+        sim.episode_totals(tot_ep, tot_ret, tot_suc)
+        return totals(tot_ep, tot_ret, tot_suc)      # RCCL all-gather over xGMI when world > 1
+
     def one_step(k, ev=None):
         if pol is not None:
-            pol.act(obs, out=act, sample=True, seed=1000 * rank, step=k)
+            pol.act(obs, out=act, sample=args.policy == "random-mlp", seed=SEED_ACT, step=k,
+                    env_offset=shard.env_offset)
         else:
-            sim.random_actions(act, 1000 * rank, k)
+            sim.random_actions(act, SEED_ACT, k)
         if ev is not None:
             ev[0].record()
-        sim.step(act, obs, rew, done, goal, autoreset=True, seed=seed)
+        sim.step(act, obs, rew, done, goal, autoreset=True, seed=SEED_RESET)
         if ev is not None:
             ev[1].record()
         if depth is not None:
@@ -184,12 +265,14 @@ def main():
             sim.render_depth(depth, cam)
             if ev is not None:
                 ev[3].record()
-        if (k + 1) % sim.horizon == 0:       # every env finished an episode this step
-            sim.episode_stats(last_ret, last_goal)
-            gather(last_ret, last_goal)      # RCCL all-gather over xGMI when world > 1
+        if (k + 1) % sim.horizon == 0:
+            gather()
 
-    for k in range(args.warmup):
+    preroll = sim.horizon if args.preroll < 0 else args.preroll
+    for k in range(preroll + args.warmup):
         one_step(k)
+    e0, r0, s0 = (x.clone() for x in gather())
+    sim.clear_status()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -197,17 +280,23 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        one_step(args.warmup + k, events[k])
+        one_step(preroll + args.warmup + k, events[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
+    kern = [e[0].elapsed_time(e[1]) for e in events]
+    kern_ms = sum(kern) / args.steps
     depth_ms = sum(e[2].elapsed_time(e[3]) for e in events) / args.steps if depth is not None else None
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    e1, r1, s1 = gather()
+    sim.status(sticky=sticky)
+    n_over = int(((sticky & _native.ST_OVERFLOW) != 0).sum())
+    n_nan = int(((sticky & (_native.ST_BADQPOS | _native.ST_BADQVEL | _native.ST_BADQACC)) != 0).sum())
+    t = torch.tensor([elapsed, kern_ms, n_over, n_nan], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms = float(t[0]), float(t[1])
+        dist.all_reduce(t[:2], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[2:], op=dist.ReduceOp.SUM)
+    elapsed, kern_ms, n_over, n_nan = float(t[0]), float(t[1]), int(t[2]), int(t[3])
     finite = bool(torch.isfinite(obs).all())
 
     if rank == 0:
@@ -216,28 +305,41 @@ def main():
         flops, counts = perfmodel.step_flops(env_id, m, sim.frame_skip)
         achieved = flops * n / (kern_ms * 1e-3) / 1e12
         bytes_step = perfmodel.step_bytes(sim.nq, sim.nv, sim.nu, sim.obs_dim, sim.nparam)
-        traffic = pmc_traffic(n)
-        roof = dict(bound="mfma", achieved=round(achieved, 3), peak=perfmodel.PEAK_FP32_TFLOPS,
+        traffic, pmc_src = pmc_traffic(n)
+        roof = dict(bound="valu", achieved=round(achieved, 3), peak=perfmodel.PEAK_FP32_TFLOPS,
                     unit="TFLOP/s", frac=round(achieved / perfmodel.PEAK_FP32_TFLOPS, 5), traffic=traffic,
                     kernel=f"k_step<{sim.nv}>", kernel_ms=round(kern_ms, 4),
+                    kernel_ms_min_max=[round(min(kern), 4), round(max(kern), 4)],
                     flops_per_env_step=round(flops), bytes_per_env_step=bytes_step,
-                    hbm_achieved_GBps=round(bytes_step * n / (kern_ms * 1e-3) / 1e9, 2),
-                    hbm_frac=round(bytes_step * n / (kern_ms * 1e-3) / 1e9 / perfmodel.PEAK_HBM_GBPS, 6),
-                    note="fp32 compute roofline (VALU == f32 MFMA peak on gfx950); FLOPs from "
-                         "perfmodel.py on profiles/work_counts_hammer.json")
-        workload = (f"{env_id}, {n} envs per GPU (north-star config), random policy, auto-reset at horizon "
-                    f"{sim.horizon}, RCCL all-gather of episode returns at episode ends")
+                    hbm_algorithmic_GBps=round(bytes_step * n / (kern_ms * 1e-3) / 1e9, 2),
+                    hbm_measured_GBps=round(traffic / (kern_ms * 1e-3) / 1e9, 2) if traffic else None,
+                    hbm_measured_frac=round(traffic / (kern_ms * 1e-3) / 1e9 / perfmodel.PEAK_HBM_GBPS, 6)
+                    if traffic else None, pmc_source=pmc_src,
+                    note="FP32 VALU roofline (157.3 TFLOP/s vector peak; the kernel issues no MFMA); FLOPs "
+                         "from perfmodel.py on profiles/work_counts_hammer.json. The HBM figures are far from "
+                         "8 TB/s by construction: ~1.1 KB compulsory traffic per env-step (SURVEY 8d), the "
+                         "north-star's 40 % of HBM roofline is unreachable on algorithmic bytes")
+        workload = (f"{env_id}, {n} envs per GPU (north-star config), random policy, staggered episode phases "
+                    f"(+{preroll}-step untimed pre-roll): auto-reset of ~{n // sim.horizon} envs per step inside "
+                    f"the timed region; per-env episode totals all-gathered every {sim.horizon} steps")
         if pol is not None:
             workload = workload.replace("random policy", "closed loop with the on-device Gaussian MLP policy "
-                                        "(mjrl MLP 32x32, random init, sampled actions)")
+                                        + ("(mjrl MLP 32x32, random init, sampled actions)"
+                                           if args.policy == "random-mlp" else
+                                           "(the reference's pretrained DAPG policy, mean actions)"))
         if depth is not None:
-            workload = (f"{env_id} + 64x64 depth-camera obs (HIP ray caster, BASELINE config 5), {n} envs per "
-                        f"GPU, random policy, auto-reset at horizon {sim.horizon}")
+            workload = workload.replace("random policy", "random policy + 64x64 depth-camera obs (HIP ray "
+                                        "caster, BASELINE config 5)")
             roof["depth_kernel_ms"] = round(depth_ms, 4)
         workload += ", MPR collider in " + ("fp64" if mpr64 else "fp32")
         metric = "env-steps/sec at N parallel envs, hammer-v0, 1/2/4/8 MI355X"
         if env_id != "hammer-v0":   # BASELINE config 3 lines are labelled with their own task
             metric = f"env-steps/sec at N parallel envs, {env_id}, 1/2/4/8 MI355X"
+        de = e1.long() - e0.long()
+        ne = int(de.sum())
+        episodes = dict(finished_in_timed_window=ne,
+                        mean_return=round(float((r1 - r0).double().sum()) / max(ne, 1), 3),
+                        success_pct=round(100.0 * int((s1 - s0).sum()) / max(ne, 1), 3))
         line = dict(metric=metric,
                     value=round(value, 1), unit="env-steps/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(elapsed / args.steps * 1e3, 4),
@@ -245,14 +347,21 @@ def main():
                     dtype="f32",
                     data="synthetic (Philox U(-1,1) actions, reference reset distribution)",
                     config=dict(workload=workload, envs_per_gpu=n, total_envs=world * n,
-                                frame_skip=sim.frame_skip, parallelism=f"env-shard x{world}"),
-                    roofline=roof, finite=finite)
+                                frame_skip=sim.frame_skip, parallelism=f"env-shard x{world}", preroll=preroll),
+                    roofline=roof, finite=finite, overflow_envs=n_over, bad_state_envs=n_nan,
+                    capacities=dict(maxcon=sim.maxcon, maxefc=sim.maxefc, maxdense=sim.maxdense),
+                    episodes=episodes)
+        if world == 1 and not args.no_parity:
+            try:
+                line["parity_one_step"] = same_run_parity(blob, env_id, sim, local)
+            except Exception as e:
+                line["parity_one_step"] = dict(error=str(e))
         if world == 1 and env_id == ENV_ID and depth is None and pol is None and n == 65536 and args.mpr == "task" \
                 and not args.no_config2:
             line["config2_4096_envs"] = config2(blob, env_id, local)
         if world == 1 and not args.no_cpu_baseline:
             try:
-                line["cpu_baseline"] = cpu_baseline(blob, env_id)
+                line["cpu_baseline"] = cpu_baseline(blob, env_id, local)
             except Exception as e:  # the baseline must not hide the GPU number
                 line["cpu_baseline"] = dict(value=None, error=str(e))
         print(json.dumps(line), flush=True)

@@ -53,11 +53,13 @@ enum {
   AW_ST_EFC_OVERFLOW = 16
 };
 
-/* aw_dims() output order */
+/* aw_dims() output order.  MAXCON / MAXEFC / MAXDENSE: the kernel's per-env capacities for
+ * contacts, constraint rows and dense (contact) rows; the reference's are nconmax 100 /
+ * njmax 500 (DAPG_assets.xml:4).  A step that needs more raises AW_ST_*_OVERFLOW. */
 enum {
   AW_DIM_NQ, AW_DIM_NV, AW_DIM_NU, AW_DIM_OBS, AW_DIM_NPARAM, AW_DIM_FRAME_SKIP,
   AW_DIM_HORIZON, AW_DIM_TASK, AW_DIM_NENV, AW_DIM_NBODY, AW_DIM_NSITE, AW_DIM_NGEOM,
-  AW_DIM_NPAIR, AW_NDIMS
+  AW_DIM_NPAIR, AW_DIM_MAXCON, AW_DIM_MAXEFC, AW_DIM_MAXDENSE, AW_NDIMS
 };
 
 /* model table = Model.to_blob() of mj_envs_amd/mjcf.py with the task block attached
@@ -75,7 +77,7 @@ int aw_set_option(aw_handle* h, int disableflags, int iterations, int noslip_ite
 
 /* Reset envs (mask[e] != 0, or all if mask == NULL): qpos = qpos0, qvel = 0, warmstart = 0,
  * per-env model params from `params` [N][nparam] or, if NULL, sampled on device (Philox,
- * keyed by seed, env index and episode count) from the reference reset distribution;
+ * keyed by seed, global env id and episode count) from the reference reset distribution;
  * then mj_forward.  obs (may be NULL) receives the reset observation. */
 int aw_reset(aw_handle* h, const uint8_t* mask, const float* params, uint64_t seed, float* obs,
              void* stream);
@@ -88,8 +90,14 @@ int aw_reset(aw_handle* h, const uint8_t* mask, const float* params, uint64_t se
 int aw_step(aw_handle* h, const float* actions, float* obs, float* reward, uint8_t* done,
             uint8_t* goal, float* terminal_obs, int autoreset, uint64_t seed, void* stream);
 
-/* i.i.d. U(-1, 1) actions from Philox (key = seed, counter = (env, step)) */
+/* i.i.d. U(-1, 1) actions from Philox (key = seed, counter = (global env id, step)) */
 int aw_random_actions(aw_handle* h, uint64_t seed, uint64_t step, float* actions, void* stream);
+
+/* Global id of this handle's env 0 (default 0).  A shard of a larger batch (one handle per
+ * GPU, envs [offset, offset + n_envs) of the global batch) sets it so every Philox stream --
+ * reset draws (aw_reset / auto-reset), aw_random_actions, aw_policy_mlp noise -- is keyed by the
+ * GLOBAL env id: N shards reproduce one unsharded run bit for bit.  Waits for the device. */
+int aw_set_env_offset(aw_handle* h, uint64_t env_offset);
 
 /* state round trip: qpos [N][nq], qvel [N][nv], warmstart [N][nv], params [N][nparam];
  * any pointer may be NULL.  set_state runs mj_forward (obs may be NULL). */
@@ -98,13 +106,28 @@ int aw_get_state(aw_handle* h, float* qpos, float* qvel, float* warmstart, float
 int aw_set_state(aw_handle* h, const float* qpos, const float* qvel, const float* warmstart,
                  const float* params, float* obs, void* stream);
 
-/* per-env status flags of the last step (AW_ST_*), uint32 [N] */
-int aw_status(aw_handle* h, uint32_t* flags, void* stream);
+/* per-env status flags (AW_ST_*), uint32 [N]: `last` = flags raised by the last step / reset /
+ * set_state of each env, `sticky` = OR of every flag raised since aw_create or the last
+ * aw_clear_status (MuJoCo's warning counters play this role); either pointer may be NULL */
+int aw_status(aw_handle* h, uint32_t* last, uint32_t* sticky, void* stream);
+int aw_clear_status(aw_handle* h, void* stream);
 
 /* completed-episode statistics: return, goal-step count, length of each env's last finished
  * episode, and the number of finished episodes; any pointer may be NULL */
 int aw_episode_stats(aw_handle* h, float* last_return, int32_t* last_goal_steps,
                      int32_t* last_len, int32_t* episodes, void* stream);
+
+/* running totals over every finished episode of each env: count, sum of returns, and count of
+ * successful episodes (> task success_steps goal steps: hammer_v0.py:167-175, pen_v0.py:180-188) */
+int aw_episode_totals(aw_handle* h, int32_t* episodes, float* sum_return, int32_t* successes,
+                      void* stream);
+
+/* episode bookkeeping of the running episode (checkpoint / resume, staggered starts): steps
+ * taken, return so far, goal steps so far, finished-episode count; any pointer may be NULL */
+int aw_get_episode(aw_handle* h, int32_t* ep_len, float* ep_ret, int32_t* ep_goal, int32_t* episodes,
+                   void* stream);
+int aw_set_episode(aw_handle* h, const int32_t* ep_len, const float* ep_ret, const int32_t* ep_goal,
+                   const int32_t* episodes, void* stream);
 
 /* Task layer only, on caller-provided kinematics for n samples (device pointers, fp32):
  * qpos [n][nq], qvel [n][nv], xpos [n][nbody][3], xquat [n][nbody][4],
@@ -117,7 +140,7 @@ int aw_task_eval(aw_handle* h, int n, const float* qpos, const float* qvel, cons
 /* Introspection for parity tests: run mj_forward (no integration) on env `env` of the
  * current state with raw control `ctrl` [nu] (NULL = 0) and copy internals into out (fp32,
  * AW_DUMP_SIZE floats; layout: mj_envs_amd/_native.py DUMP_LAYOUT). */
-#define AW_DUMP_SIZE 2728
+#define AW_DUMP_SIZE 3208
 int aw_forward_dump(aw_handle* h, int env, const float* ctrl, float* out, void* stream);
 
 /* Depth camera observation (the reference renders RGB through OpenGL:
@@ -136,11 +159,11 @@ int aw_render_depth(aw_handle* h, const float* cam, int width, int height, float
  * reference's DAPG baseline (algos/baselines.py:67-86, hidden_sizes=(32, 32)) -- two tanh
  * hidden layers of width `hidden` (32 or 64), in/out affine transforms, and with sample != 0
  * the Gaussian exploration noise exp(log_std) * N(0, 1) (Philox, key = seed, counter =
- * (env, step)); sample == 0 returns the mean (get_action(...)[1]['evaluation']).
+ * (env_offset + env, step)); sample == 0 returns the mean (get_action(...)[1]['evaluation']).
  * params: device fp32 block, layout in mj_envs_amd/csrc/aw_policy.h; obs [n][in_dim] ->
  * act [n][out_dim], in_dim <= 64, out_dim <= 32.  Stateless: no handle. */
 int aw_policy_mlp(int n, int in_dim, int hidden, int out_dim, const float* params, const float* obs,
-                  float* act, int sample, uint64_t seed, uint64_t step, void* stream);
+                  float* act, int sample, uint64_t seed, uint64_t step, uint64_t env_offset, void* stream);
 
 /* Diagnostic: per-stage shader-clock cycles of k_step summed over all waves since the last
  * reset (40 counters, see aw_common.h PR_*).  Only libraries built with -DAW_STAGE_PROF

@@ -17,17 +17,29 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # AW_LIB selects a diagnostic build (e.g. libadroit_hip_prof.so with the stage profiler)
 LIB_PATH = os.environ.get("AW_LIB") or os.path.join(HERE, "libadroit_hip.so")
 
-AW_NDIMS = 13
+AW_NDIMS = 16
 # aw_set_option bits of ours: MPR (cylinder) collider in fp32 / in fp64 (neither: the task default)
 DSBL_MPR_FP64 = 1 << 16
 DSBL_MPR_FP32 = 1 << 17
-AW_DUMP_SIZE = 2728
-# float offsets inside the aw_forward_dump output (see adroit_wave.hip k_dump)
-DUMP_LAYOUT = dict(xpos=(0, 96), xquat=(96, 128), site_xpos=(224, 96), qacc_smooth=(320, 36),
-                   qfrc_smooth=(356, 36), qacc=(392, 36), qfrc_constraint=(428, 36), qM=(464, 1296),
-                   scalars=(1760, 8), con_dist=(1768, 32), con_pos=(1800, 96), con_frame=(1896, 288),
-                   con_pair=(2184, 32), efc_force=(2216, 128), efc_aref=(2344, 128), efc_D=(2472, 128),
-                   efc_type=(2600, 128))
+# kernel capacities (aw_common.h; also reported by aw_dims)
+MAXCON, MAXEFC, MAXDENSE = 48, 192, 128
+ST_BADQPOS, ST_BADQVEL, ST_BADQACC, ST_CON_OVERFLOW, ST_EFC_OVERFLOW = 1, 2, 4, 8, 16
+ST_OVERFLOW = ST_CON_OVERFLOW | ST_EFC_OVERFLOW
+
+
+def dump_layout(maxcon=MAXCON, maxefc=MAXEFC):
+    """float offsets inside the aw_forward_dump output (adroit_wave.hip k_dump, DUMP_*)"""
+    c, e = 1768, 1768 + 14 * maxcon
+    return dict(xpos=(0, 96), xquat=(96, 128), site_xpos=(224, 96), qacc_smooth=(320, 36),
+                qfrc_smooth=(356, 36), qacc=(392, 36), qfrc_constraint=(428, 36), qM=(464, 1296),
+                scalars=(1760, 8), con_dist=(c, maxcon), con_pos=(c + maxcon, 3 * maxcon),
+                con_frame=(c + 4 * maxcon, 9 * maxcon), con_pair=(c + 13 * maxcon, maxcon),
+                efc_force=(e, maxefc), efc_aref=(e + maxefc, maxefc), efc_D=(e + 2 * maxefc, maxefc),
+                efc_type=(e + 3 * maxefc, maxefc))
+
+
+DUMP_LAYOUT = dump_layout()
+AW_DUMP_SIZE = 1768 + 14 * MAXCON + 4 * MAXEFC
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -53,9 +65,14 @@ def load():
     L.aw_reset.argtypes = [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]
     L.aw_step.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_uint64, _vp]
     L.aw_random_actions.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp]
+    L.aw_set_env_offset.argtypes = [_vp, ctypes.c_uint64]
+    L.aw_clear_status.argtypes = [_vp, _vp]
+    L.aw_episode_totals.argtypes = [_vp, _vp, _vp, _vp, _vp]
+    L.aw_get_episode.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp]
+    L.aw_set_episode.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp]
     L.aw_get_state.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp]
     L.aw_set_state.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp]
-    L.aw_status.argtypes = [_vp, _vp, _vp]
+    L.aw_status.argtypes = [_vp, _vp, _vp, _vp]
     L.aw_episode_stats.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp]
     L.aw_task_eval.argtypes = [_vp, ctypes.c_int] + [_vp] * 10 + [_vp]
     L.aw_forward_dump.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp]
@@ -67,19 +84,22 @@ def load():
         L.aw_render_depth.restype = ctypes.c_int
     if hasattr(L, "aw_policy_mlp"):
         L.aw_policy_mlp.argtypes = [ctypes.c_int] * 4 + [_vp, _vp, _vp, ctypes.c_int, ctypes.c_uint64,
-                                                         ctypes.c_uint64, _vp]
+                                                         ctypes.c_uint64, ctypes.c_uint64, _vp]
         L.aw_policy_mlp.restype = ctypes.c_int
     for f in ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "aw_step",
               "aw_random_actions", "aw_get_state", "aw_set_state", "aw_status", "aw_episode_stats",
-              "aw_task_eval", "aw_forward_dump", "aw_stage_profile"):
+              "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_set_env_offset", "aw_clear_status",
+              "aw_episode_totals", "aw_get_episode", "aw_set_episode"):
         getattr(L, f).restype = ctypes.c_int
     _lib = L
     return L
 
 
 EXPORTS = ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "aw_step",
-           "aw_random_actions", "aw_get_state", "aw_set_state", "aw_status", "aw_episode_stats",
-           "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_render_depth", "aw_policy_mlp", "aw_last_error")
+           "aw_random_actions", "aw_set_env_offset", "aw_get_state", "aw_set_state", "aw_status",
+           "aw_clear_status", "aw_episode_stats", "aw_episode_totals", "aw_get_episode", "aw_set_episode",
+           "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_render_depth", "aw_policy_mlp",
+           "aw_last_error")
 
 STAGES = ("pre", "kinematics", "collision", "com_crb", "rne_smooth_solve", "constraints", "newton",
           "noslip", "jt_touch", "euler", "task_obs", "reset", "checks")
@@ -119,7 +139,7 @@ def _stream():
 class Sim:
     """One batch of ``n_envs`` envs of one task on one GPU (owns the device state)."""
 
-    def __init__(self, blob: bytes, n_envs: int, device: int = 0):
+    def __init__(self, blob: bytes, n_envs: int, device: int = 0, env_offset: int = 0):
         import torch
         L = load()
         self.device = device
@@ -132,7 +152,16 @@ class Sim:
         d = (ctypes.c_int * AW_NDIMS)()
         _check(L.aw_dims(self.h, d))
         (self.nq, self.nv, self.nu, self.obs_dim, self.nparam, self.frame_skip, self.horizon,
-         self.task_kind, self.n_envs, self.nbody, self.nsite, self.ngeom, self.npair) = list(d)
+         self.task_kind, self.n_envs, self.nbody, self.nsite, self.ngeom, self.npair,
+         self.maxcon, self.maxefc, self.maxdense) = list(d)
+        self.env_offset = 0
+        if env_offset:
+            self.set_env_offset(env_offset)
+
+    def set_env_offset(self, env_offset: int):
+        """global id of env 0 (shards): Philox streams are keyed by the global env id"""
+        _check(load().aw_set_env_offset(self.h, int(env_offset)))
+        self.env_offset = int(env_offset)
 
     def close(self):
         if getattr(self, "h", None):
@@ -171,8 +200,23 @@ class Sim:
         _check(load().aw_set_state(self.h, _ptr(qpos), _ptr(qvel), _ptr(warm), _ptr(params), _ptr(obs),
                                    _stream()))
 
-    def status(self, out):
-        _check(load().aw_status(self.h, _ptr(out), _stream()))
+    def status(self, last=None, sticky=None):
+        """per-env flags (ST_*): of the last step (last) / OR since create or clear_status (sticky)"""
+        _check(load().aw_status(self.h, _ptr(last), _ptr(sticky), _stream()))
+
+    def clear_status(self):
+        _check(load().aw_clear_status(self.h, _stream()))
+
+    def episode_totals(self, episodes=None, sum_return=None, successes=None):
+        _check(load().aw_episode_totals(self.h, _ptr(episodes), _ptr(sum_return), _ptr(successes), _stream()))
+
+    def get_episode(self, ep_len=None, ep_ret=None, ep_goal=None, episodes=None):
+        _check(load().aw_get_episode(self.h, _ptr(ep_len), _ptr(ep_ret), _ptr(ep_goal), _ptr(episodes),
+                                     _stream()))
+
+    def set_episode(self, ep_len=None, ep_ret=None, ep_goal=None, episodes=None):
+        _check(load().aw_set_episode(self.h, _ptr(ep_len), _ptr(ep_ret), _ptr(ep_goal), _ptr(episodes),
+                                     _stream()))
 
     def episode_stats(self, last_return=None, last_goal=None, last_len=None, episodes=None):
         _check(load().aw_episode_stats(self.h, _ptr(last_return), _ptr(last_goal), _ptr(last_len),

@@ -40,6 +40,9 @@ struct DState {
   float* qpos; float* qvel; float* warm; float* params;
   int* ep_len; float* ep_ret; int* ep_goal; int* episode; unsigned* status;
   float* last_ret; int* last_goal; int* last_len;
+  unsigned* status_acc;   // OR of every step's flags since create / aw_clear_status (sticky)
+  float* sum_ret;         // sum of the returns of every finished episode
+  int* n_success;         // finished episodes with > success_steps goal steps (evaluate_success)
 };
 
 // ---------------------------------------------------------------------------------------
@@ -181,7 +184,7 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV], Dof& d
     AW_PROF(s, PR_NOSLIP);
     for (int r = lane; r < s.nefc; r += 64) s.rowbuf[r] = s.efc_force[r];
     wsync();
-    float qc = jt_mul<NV>(s, lane);
+    float qc = jt_mul<NV>(m, s, lane);
     d.qacc = lane < NV ? a : 0.f;
     d.qfrc_con = lane < NV ? qc : 0.f;
   }
@@ -218,9 +221,12 @@ AW_DEV void euler(const DModel& m, Env& s, int lane, const float (&Mrow)[NV], co
   wsync();
 }
 
+// mj_resetData on the state: qpos0 (= 0 for these models), qvel, warmstart and ctrl zeroed --
+// after a bad-state reset inside an env-step, the remaining substeps run with ctrl = 0, as the
+// reference's do_simulation writes ctrl once before its frame_skip mj_step calls
 template <int NV>
 AW_DEV void reset_state(Env& s, int lane) {
-  if (lane < NV) { s.qpos[lane] = 0.f; s.qvel[lane] = 0.f; s.warm[lane] = 0.f; }
+  if (lane < NV) { s.qpos[lane] = 0.f; s.qvel[lane] = 0.f; s.warm[lane] = 0.f; s.ctrl[lane] = 0.f; }
   wsync();
 }
 
@@ -256,7 +262,7 @@ AW_DEV void load_env(const DModel& m, Env& s, const DState& st, int env, int lan
     s.qvel[lane] = st.qvel[(size_t)env * m.nv + lane];
     s.warm[lane] = st.warm[(size_t)env * m.nv + lane];
   }
-  if (lane == 0) s.status = 0u;
+  if (lane == 0) { s.status = 0u; s.env = env; }
 }
 template <int NV>
 AW_DEV void store_env(const DModel& m, Env& s, const DState& st, int env, int lane) {
@@ -283,7 +289,9 @@ AW_DEV void reset_prepare(const DModel& m, Env& s, const DState& st, int env, in
       for (int p = 0; p < m.nparam; p++) prm[p] = params_in[(size_t)env * m.nparam + p];
     } else {
       float tmp[MAXP];
-      sample_params(m, seed, (uint32_t)env, (uint32_t)st.episode[env], tmp);
+#pragma unroll
+      for (int p = 0; p < MAXP; p++) tmp[p] = p < m.nparam ? prm[p] : 0.f;
+      sample_params(m, seed, (uint32_t)(m.env_offset + (unsigned long long)env), (uint32_t)st.episode[env], tmp);
 #pragma unroll
       for (int p = 0; p < MAXP; p++)
         if (p < m.nparam) prm[p] = tmp[p];
@@ -384,11 +392,14 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
       st.ep_ret[env] = ret;
       st.ep_goal[env] = gcount;
       st.status[env] = s.status;
+      st.status_acc[env] |= s.status;
       if (term || trunc) {
         st.last_ret[env] = ret;
         st.last_goal[env] = gcount;
         st.last_len[env] = t;
         st.episode[env] += 1;
+        st.sum_ret[env] += ret;
+        st.n_success[env] += gcount > m.success_steps ? 1 : 0;
       }
     }
     store_env<NV>(m, s, st, env, lane);
@@ -406,6 +417,7 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
   if (resetting) {
     write_obs(m, s, lane, ob);
     store_env<NV>(m, s, st, env, lane);
+    if (lane == 0) st.status_acc[env] |= s.status;
   }
 #ifdef AW_STAGE_PROF
   AW_PROF(s, PR_TASK);
@@ -422,9 +434,10 @@ __global__ void __launch_bounds__(64) k_reset(DModel m, DState st, int n, const 
   const int env = blockIdx.x, lane = threadIdx.x;
   if (env >= n) return;
   if (mask && !mask[env]) return;
-  if (lane == 0) s.status = 0u;
+  if (lane == 0) { s.status = 0u; s.env = env; }
   reset_env<NV, MP>(m, s, st, env, lane, params, seed, obs);
   store_env<NV>(m, s, st, env, lane);
+  if (lane == 0) { st.status[env] = s.status; st.status_acc[env] |= s.status; }
 }
 
 template <int NV, int MP>
@@ -450,9 +463,12 @@ __global__ void __launch_bounds__(64) k_set_state(DModel m, DState st, int n, co
   forward<NV, MP>(m, s, lane, Mrow, d);
   if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
   store_env<NV>(m, s, st, env, lane);
+  if (lane == 0) { st.status[env] = s.status; st.status_acc[env] |= s.status; }
 }
 
-// dump layout (floats): see mj_envs_amd/_native.py DUMP_LAYOUT
+// dump layout (floats): see mj_envs_amd/_native.py dump_layout (same offsets from the capacities)
+constexpr int DUMP_SCAL = 1760, DUMP_CON = 1768, DUMP_EFC = DUMP_CON + 14 * MAXCON;
+static_assert(DUMP_EFC + 4 * MAXEFC == AW_DUMP_SIZE, "AW_DUMP_SIZE out of date");
 template <int NV, int MP>
 __global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const float* ctrl, float* out) {
   __shared__ Env s;
@@ -476,26 +492,26 @@ __global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const
   for (int k = 0; k < NV; k++)
     if (lane < NV) out[464 + lane * NV + k] = Mrow[k];
   if (lane == 0) {
-    out[1760] = (float)s.ncon; out[1761] = (float)s.nefc; out[1762] = (float)s.nsparse;
-    out[1763] = (float)s.ndense; out[1764] = s.touch[0]; out[1765] = (float)s.status;
-    out[1766] = (float)s.it_newton; out[1767] = (float)s.it_noslip;
+    out[DUMP_SCAL] = (float)s.ncon; out[DUMP_SCAL + 1] = (float)s.nefc; out[DUMP_SCAL + 2] = (float)s.nsparse;
+    out[DUMP_SCAL + 3] = (float)s.ndense; out[DUMP_SCAL + 4] = s.touch[0]; out[DUMP_SCAL + 5] = (float)s.status;
+    out[DUMP_SCAL + 6] = (float)s.it_newton; out[DUMP_SCAL + 7] = (float)s.it_noslip;
   }
   if (lane < MAXCON) {
     bool v = lane < s.ncon;
-    out[1768 + lane] = v ? s.con_dist[lane] : 0.f;
-    for (int k = 0; k < 3; k++) out[1800 + 3 * lane + k] = v ? s.con_pos[lane][k] : 0.f;
+    out[DUMP_CON + lane] = v ? s.con_dist[lane] : 0.f;
+    for (int k = 0; k < 3; k++) out[DUMP_CON + MAXCON + 3 * lane + k] = v ? s.con_pos[lane][k] : 0.f;
     float fr[9];
     for (int k = 0; k < 3; k++) { fr[k] = v ? s.con_nrm[lane][k] : 1.f; fr[3 + k] = 0.f; }
     make_frame(fr);
-    for (int k = 0; k < 9; k++) out[1896 + 9 * lane + k] = v ? fr[k] : 0.f;
-    out[2184 + lane] = v ? (float)s.con_pair[lane] : -1.f;
+    for (int k = 0; k < 9; k++) out[DUMP_CON + 4 * MAXCON + 9 * lane + k] = v ? fr[k] : 0.f;
+    out[DUMP_CON + 13 * MAXCON + lane] = v ? (float)s.con_pair[lane] : -1.f;
   }
   for (int r = lane; r < MAXEFC; r += 64) {
     bool v = r < s.nefc;
-    out[2216 + r] = v ? s.efc_force[r] : 0.f;
-    out[2344 + r] = v ? s.efc_aref[r] : 0.f;
-    out[2472 + r] = v ? s.efc_D[r] : 0.f;
-    out[2600 + r] = v ? (float)s.efc_type[r] : -1.f;
+    out[DUMP_EFC + r] = v ? s.efc_force[r] : 0.f;
+    out[DUMP_EFC + MAXEFC + r] = v ? s.efc_aref[r] : 0.f;
+    out[DUMP_EFC + 2 * MAXEFC + r] = v ? s.efc_D[r] : 0.f;
+    out[DUMP_EFC + 3 * MAXEFC + r] = v ? (float)s.efc_type[r] : -1.f;
   }
 }
 
@@ -546,11 +562,12 @@ __global__ void __launch_bounds__(256) k_depth(DModel m, DState st, int n, CamRe
   for (int p0 = (tid >> 6) * 64; p0 < W * H; p0 += 256) render_span(rg, m.nrgeom, cam.c, W, H, p0, lane, o);
 }
 
-__global__ void k_random_actions(int n, int nu, uint64_t seed, uint64_t step, float* out) {
+__global__ void k_random_actions(int n, int nu, uint64_t seed, uint64_t step, uint64_t env_offset, float* out) {
   int env = blockIdx.x * blockDim.x + threadIdx.x;
   if (env >= n) return;
+  const uint32_t genv = (uint32_t)(env_offset + (uint64_t)env);   // global env id (shard offset)
   for (int blk = 0; blk * 4 < nu; blk++) {
-    uint32_t c[4] = {(uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), (uint32_t)blk};
+    uint32_t c[4] = {genv, (uint32_t)step, (uint32_t)(step >> 32), (uint32_t)blk};
     philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
     for (int k = 0; k < 4 && blk * 4 + k < nu; k++) out[(size_t)env * nu + blk * 4 + k] = 2.f * u01(c[k]) - 1.f;
   }
@@ -641,6 +658,7 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
   m.tar_length = (float)B.opt("task_tar_length", 1);
   m.task_kind = B.dim("task_kind"); m.frame_skip = B.dim("task_frame_skip", 1);
   m.horizon = B.dim("task_horizon", 0); m.obs_dim = B.dim("task_obs_dim", 0);
+  m.success_steps = B.dim("task_success_steps", 25);
   m.nparam = B.dim("task_nparam", 0); m.variation = B.dim("task_variation", 0);
   if (m.nparam > MAXP) return fail(AW_EUNSUPPORTED, "too many per-env params");
   m.disableflags = 0;
@@ -815,7 +833,7 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
     }
     m.cls_start[0] = 0;
     for (int c = 0; c < NCLASS; c++) m.cls_start[c + 1] = m.cls_start[c] + ccount[c];
-    if (m.npairall > MAXDENSE * VS * 2) return fail(AW_EUNSUPPORTED, "too many collision pairs");
+    if (m.npairall > JL * VS * 2) return fail(AW_EUNSUPPORTED, "too many collision pairs");
     PUT(cp_class, pcls); PUT(cp_rb, prb);
     std::vector<int> ppack(m.npairall);
     for (int p = 0; p < m.npairall; p++) ppack[p] = pcls[p] | (pg1[p] << 8) | (pg2[p] << 16);
@@ -890,6 +908,7 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
   PUT(task_idx, tidx); PUT(param_field, pf); PUT(param_obj, po); PUT(param_comp, pc);
   PUT(act_mid, tof(B.f("task_act_mid"))); PUT(act_rng, tof(B.f("task_act_rng")));
   PUT(param_default, tof(B.f("task_param_default")));
+  PUT(param_draw, B.i("task_param_draw"));
   std::vector<double> dlo = B.f("task_draw_lo"), dhi = B.f("task_draw_hi");
   m.ndraw = (int)dlo.size();
   if (m.ndraw > 8) return fail(AW_EUNSUPPORTED, "too many reset draws");
@@ -951,64 +970,67 @@ extern "C" {
 
 const char* aw_last_error(void) { return g_err.c_str(); }
 
+static void free_handle(aw_handle* h) {
+  if (!h) return;
+  if (h->dmodel) (void)hipFree(h->dmodel);
+  if (h->dmhdr) (void)hipFree(h->dmhdr);
+  if (h->dstate) (void)hipFree(h->dstate);
+  if (h->m.jspill) (void)hipFree(h->m.jspill);
+  delete h;
+}
+
+// carve the per-env state arrays out of one allocation (each 256-byte aligned)
+static size_t layout_state(aw_handle* h, char* base) {
+  size_t N = (size_t)h->nenv, nq = h->m.nq, nv = h->m.nv, np = std::max(h->m.nparam, 1);
+  uintptr_t p = (uintptr_t)base;   // base == nullptr: dry run, only the size is used
+  auto take = [&](size_t b) { uintptr_t r = p; p += (b + 255) & ~size_t(255); return (char*)r; };
+  DState& st = h->st;
+  st.qpos = (float*)take(N * nq * 4); st.qvel = (float*)take(N * nv * 4); st.warm = (float*)take(N * nv * 4);
+  st.params = (float*)take(N * np * 4); st.ep_len = (int*)take(N * 4); st.ep_ret = (float*)take(N * 4);
+  st.ep_goal = (int*)take(N * 4); st.episode = (int*)take(N * 4); st.status = (unsigned*)take(N * 4);
+  st.last_ret = (float*)take(N * 4); st.last_goal = (int*)take(N * 4); st.last_len = (int*)take(N * 4);
+  st.status_acc = (unsigned*)take(N * 4); st.sum_ret = (float*)take(N * 4); st.n_success = (int*)take(N * 4);
+  return (size_t)(p - (uintptr_t)base);
+}
+
 int aw_create(const void* blob, size_t nbytes, int n_envs, int device, aw_handle** out) {
   if (!blob || !out || n_envs <= 0) return fail(AW_EINVAL, "aw_create: bad arguments");
+  *out = nullptr;
   Blob B{blob, nbytes};
-  aw_handle* h = new aw_handle();
+  std::unique_ptr<aw_handle, void (*)(aw_handle*)> h(new aw_handle(), free_handle);
   h->device = device;
   h->nenv = n_envs;
   std::unique_ptr<MData> md(new MData());   // value-initialised: zero
-  int rc = build_model(B, h->m, *md);
-  if (rc) { delete h; return rc; }
+  if (int rc = build_model(B, h->m, *md)) return rc;
   h->NV = h->m.nv;
   h->mpr_fp64 = B.dim("task_mpr_fp64", 1);   // no task block: MuJoCo's fp64
-  if (h->NV != 30 && h->NV != 33 && h->NV != 36) { delete h; return fail(AW_EUNSUPPORTED, "nv not instantiated"); }
+  if (h->NV != 30 && h->NV != 33 && h->NV != 36) return fail(AW_EUNSUPPORTED, "nv not instantiated");
   HIPCHK(hipSetDevice(device));
   HIPCHK(hipMalloc(&h->dmodel, sizeof(MData)));
   HIPCHK(hipMemcpy(h->dmodel, md.get(), sizeof(MData), hipMemcpyHostToDevice));
   h->m.d = (const MData*)h->dmodel;
+  HIPCHK(hipMalloc((void**)&h->m.jspill, (size_t)n_envs * JSPILL * sizeof(float)));
   HIPCHK(hipMalloc(&h->dmhdr, sizeof(DModel) + sizeof(DState)));
-  // state
-  size_t N = (size_t)n_envs, nq = h->m.nq, nv = h->m.nv, np = std::max(h->m.nparam, 1);
-  size_t bytes = N * (nq + 2 * nv + np) * 4 + N * 4 * 10 + 256;
+  const size_t bytes = layout_state(h.get(), nullptr);   // dry run: sizes only
   HIPCHK(hipMalloc(&h->dstate, bytes));
   HIPCHK(hipMemset(h->dstate, 0, bytes));
-  char* p = (char*)h->dstate;
-  auto take = [&](size_t b) { char* r = p; p += (b + 255) & ~size_t(255); return r; };
-  h->st.qpos = (float*)take(N * nq * 4); h->st.qvel = (float*)take(N * nv * 4); h->st.warm = (float*)take(N * nv * 4);
-  h->st.params = (float*)take(N * np * 4); h->st.ep_len = (int*)take(N * 4); h->st.ep_ret = (float*)take(N * 4);
-  h->st.ep_goal = (int*)take(N * 4); h->st.episode = (int*)take(N * 4); h->st.status = (unsigned*)take(N * 4);
-  h->st.last_ret = (float*)take(N * 4); h->st.last_goal = (int*)take(N * 4); h->st.last_len = (int*)take(N * 4);
-  if ((size_t)(p - (char*)h->dstate) > bytes) {
-    // re-allocate with the exact size (alignment padding)
-    size_t need = (size_t)(p - (char*)h->dstate);
-    HIPCHK(hipFree(h->dstate));
-    HIPCHK(hipMalloc(&h->dstate, need));
-    HIPCHK(hipMemset(h->dstate, 0, need));
-    p = (char*)h->dstate;
-    h->st.qpos = (float*)take(N * nq * 4); h->st.qvel = (float*)take(N * nv * 4); h->st.warm = (float*)take(N * nv * 4);
-    h->st.params = (float*)take(N * np * 4); h->st.ep_len = (int*)take(N * 4); h->st.ep_ret = (float*)take(N * 4);
-    h->st.ep_goal = (int*)take(N * 4); h->st.episode = (int*)take(N * 4); h->st.status = (unsigned*)take(N * 4);
-    h->st.last_ret = (float*)take(N * 4); h->st.last_goal = (int*)take(N * 4); h->st.last_len = (int*)take(N * 4);
-  }
+  layout_state(h.get(), (char*)h->dstate);
   // default params for every env
+  size_t N = (size_t)n_envs, np = std::max(h->m.nparam, 1);
   std::vector<float> prm(N * np, 0.f);
   std::vector<double> def = B.f("task_param_default");
   for (size_t e = 0; e < N; e++)
     for (int k = 0; k < h->m.nparam; k++) prm[e * np + k] = (float)def[k];
   HIPCHK(hipMemcpy(h->st.params, prm.data(), prm.size() * 4, hipMemcpyHostToDevice));
-  if (int rc2 = upload_header(h)) return rc2;
-  *out = h;
+  if (int rc2 = upload_header(h.get())) return rc2;
+  *out = h.release();
   return AW_OK;
 }
 
 int aw_destroy(aw_handle* h) {
   if (!h) return AW_OK;
-  hipSetDevice(h->device);
-  if (h->dmodel) hipFree(h->dmodel);
-  if (h->dmhdr) hipFree(h->dmhdr);
-  if (h->dstate) hipFree(h->dstate);
-  delete h;
+  (void)hipSetDevice(h->device);
+  free_handle(h);
   return AW_OK;
 }
 
@@ -1016,7 +1038,7 @@ int aw_dims(const aw_handle* h, int* d) {
   if (!h || !d) return fail(AW_EINVAL, "aw_dims: null");
   const DModel& m = h->m;
   int v[AW_NDIMS] = {m.nq, m.nv, m.nu, m.obs_dim, m.nparam, m.frame_skip, m.horizon, m.task_kind, h->nenv,
-                     m.nbody, m.nsite, m.ngeom, m.npairall};
+                     m.nbody, m.nsite, m.ngeom, m.npairall, MAXCON, MAXEFC, MAXDENSE};
   memcpy(d, v, sizeof(v));
   return AW_OK;
 }
@@ -1056,7 +1078,8 @@ int aw_random_actions(aw_handle* h, uint64_t seed, uint64_t step, float* actions
   if (!h || !actions) return fail(AW_EINVAL, "aw_random_actions: null");
   HIPCHK(hipSetDevice(h->device));
   int bs = 256, nb = (h->nenv + bs - 1) / bs;
-  hipLaunchKernelGGL(k_random_actions, dim3(nb), dim3(bs), 0, (hipStream_t)stream, h->nenv, h->m.nu, seed, step, actions);
+  hipLaunchKernelGGL(k_random_actions, dim3(nb), dim3(bs), 0, (hipStream_t)stream, h->nenv, h->m.nu, seed, step,
+                     (uint64_t)h->m.env_offset, actions);
   HIPCHK(hipGetLastError());
   return AW_OK;
 }
@@ -1085,10 +1108,64 @@ int aw_set_state(aw_handle* h, const float* qpos, const float* qvel, const float
   return AW_OK;
 }
 
-int aw_status(aw_handle* h, uint32_t* flags, void* stream) {
-  if (!h || !flags) return fail(AW_EINVAL, "aw_status: null");
+int aw_status(aw_handle* h, uint32_t* last, uint32_t* sticky, void* stream) {
+  if (!h || (!last && !sticky)) return fail(AW_EINVAL, "aw_status: null");
   HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipMemcpyAsync(flags, h->st.status, (size_t)h->nenv * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  const size_t b = (size_t)h->nenv * 4;
+  if (last) HIPCHK(hipMemcpyAsync(last, h->st.status, b, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  if (sticky) HIPCHK(hipMemcpyAsync(sticky, h->st.status_acc, b, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return AW_OK;
+}
+
+int aw_clear_status(aw_handle* h, void* stream) {
+  if (!h) return fail(AW_EINVAL, "aw_clear_status: null");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipMemsetAsync(h->st.status_acc, 0, (size_t)h->nenv * 4, (hipStream_t)stream));
+  return AW_OK;
+}
+
+int aw_set_env_offset(aw_handle* h, uint64_t env_offset) {
+  if (!h) return fail(AW_EINVAL, "aw_set_env_offset: null");
+  h->m.env_offset = env_offset;
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipDeviceSynchronize());   // steps already queued read the old header
+  return upload_header(h);
+}
+
+int aw_get_episode(aw_handle* h, int32_t* ep_len, float* ep_ret, int32_t* ep_goal, int32_t* episodes,
+                   void* stream) {
+  if (!h) return fail(AW_EINVAL, "aw_get_episode: null");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t b = (size_t)h->nenv * 4;
+  if (ep_len) HIPCHK(hipMemcpyAsync(ep_len, h->st.ep_len, b, hipMemcpyDeviceToDevice, st));
+  if (ep_ret) HIPCHK(hipMemcpyAsync(ep_ret, h->st.ep_ret, b, hipMemcpyDeviceToDevice, st));
+  if (ep_goal) HIPCHK(hipMemcpyAsync(ep_goal, h->st.ep_goal, b, hipMemcpyDeviceToDevice, st));
+  if (episodes) HIPCHK(hipMemcpyAsync(episodes, h->st.episode, b, hipMemcpyDeviceToDevice, st));
+  return AW_OK;
+}
+
+int aw_set_episode(aw_handle* h, const int32_t* ep_len, const float* ep_ret, const int32_t* ep_goal,
+                   const int32_t* episodes, void* stream) {
+  if (!h) return fail(AW_EINVAL, "aw_set_episode: null");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t b = (size_t)h->nenv * 4;
+  if (ep_len) HIPCHK(hipMemcpyAsync(h->st.ep_len, ep_len, b, hipMemcpyDeviceToDevice, st));
+  if (ep_ret) HIPCHK(hipMemcpyAsync(h->st.ep_ret, ep_ret, b, hipMemcpyDeviceToDevice, st));
+  if (ep_goal) HIPCHK(hipMemcpyAsync(h->st.ep_goal, ep_goal, b, hipMemcpyDeviceToDevice, st));
+  if (episodes) HIPCHK(hipMemcpyAsync(h->st.episode, episodes, b, hipMemcpyDeviceToDevice, st));
+  return AW_OK;
+}
+
+int aw_episode_totals(aw_handle* h, int32_t* episodes, float* sum_return, int32_t* successes, void* stream) {
+  if (!h) return fail(AW_EINVAL, "aw_episode_totals: null");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t b = (size_t)h->nenv * 4;
+  if (episodes) HIPCHK(hipMemcpyAsync(episodes, h->st.episode, b, hipMemcpyDeviceToDevice, st));
+  if (sum_return) HIPCHK(hipMemcpyAsync(sum_return, h->st.sum_ret, b, hipMemcpyDeviceToDevice, st));
+  if (successes) HIPCHK(hipMemcpyAsync(successes, h->st.n_success, b, hipMemcpyDeviceToDevice, st));
   return AW_OK;
 }
 
@@ -1140,14 +1217,14 @@ int aw_render_depth(aw_handle* h, const float* cam, int width, int height, float
 }
 
 int aw_policy_mlp(int n, int in_dim, int hidden, int out_dim, const float* params, const float* obs, float* act,
-                  int sample, uint64_t seed, uint64_t step, void* stream) {
+                  int sample, uint64_t seed, uint64_t step, uint64_t env_offset, void* stream) {
   if (n <= 0 || !params || !obs || !act || in_dim <= 0 || in_dim > MLP_IMAX || out_dim <= 0 || out_dim > MLP_OMAX)
     return fail(AW_EINVAL, "aw_policy_mlp: bad arguments");
   const int bs = 256, nb = (n + bs - 1) / bs;
   hipStream_t st = (hipStream_t)stream;
   switch (hidden) {
-    case 32: hipLaunchKernelGGL(k_mlp<32>, dim3(nb), dim3(bs), 0, st, n, in_dim, out_dim, params, obs, act, sample, seed, step); break;
-    case 64: hipLaunchKernelGGL(k_mlp<64>, dim3(nb), dim3(bs), 0, st, n, in_dim, out_dim, params, obs, act, sample, seed, step); break;
+    case 32: hipLaunchKernelGGL(k_mlp<32>, dim3(nb), dim3(bs), 0, st, n, in_dim, out_dim, params, obs, act, sample, seed, step, env_offset); break;
+    case 64: hipLaunchKernelGGL(k_mlp<64>, dim3(nb), dim3(bs), 0, st, n, in_dim, out_dim, params, obs, act, sample, seed, step, env_offset); break;
     default: return fail(AW_EUNSUPPORTED, "aw_policy_mlp: hidden width must be 32 or 64 (two hidden layers)");
   }
   HIPCHK(hipGetLastError());

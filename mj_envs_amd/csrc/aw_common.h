@@ -21,9 +21,17 @@ constexpr int MAXG = 36;      // collidable geoms (compact list)
 constexpr int MAXS = 32;      // sites
 constexpr int MAXT = 44;      // tendons
 constexpr int MAXU = 30;      // actuators
-constexpr int MAXCON = 32;    // contacts kept per env (oracle uses the same cap)
-constexpr int MAXEFC = 128;   // constraint rows
-constexpr int MAXDENSE = 48;  // dense (contact) constraint rows: 12 pyramidal condim-3 contacts
+// Constraint capacities.  Sized from the oracle's work counts at MuJoCo's own capacities
+// (nconmax 100 / njmax 500, DAPG_assets.xml:4) under the reference's pretrained DAPG policies
+// (profiles/work_counts_*_dapg.json: max ncon 20, nefc 130, dense rows 98 over 4 tasks x 32
+// envs x one horizon): 2.4x / 1.5x / 1.3x headroom.  Overflow still raises ST_*_OVERFLOW.
+constexpr int MAXCON = 48;    // contacts per env (one lane each in the sort)
+constexpr int NRL = 3;        // constraint rows per lane in the Newton solver
+constexpr int MAXEFC = 64 * NRL;  // constraint rows (192)
+constexpr int MAXDENSE = 128; // dense (contact) rows: noslip keeps <= 64 opposing edge pairs, one per lane
+constexpr int JL = 32;        // dense J rows kept in LDS; rows [JL, MAXDENSE) live in the env's global
+                              // spill block (DModel::jspill), read back through L1 / L2
+constexpr int JSPILL = (MAXDENSE - JL) * VS;  // floats per env in the spill block (row stride VS)
 constexpr int MAXP = 8;       // per-env model parameters
 constexpr int MAXLEV = 16;    // kinematic tree depth
 constexpr int MAXTOUCH = 4;   // task touch sensors
@@ -136,6 +144,7 @@ constexpr int MAXRG = 64;     // rendered (primitive) geoms
   X(int, task_idx, MAXTIDX) X(int, param_field, MAXP) X(int, param_obj, MAXP)                   \
   X(int, param_comp, MAXP) X(float, act_mid, MAXU) X(float, act_rng, MAXU)                      \
   X(float, param_default, MAXP) X(float, draw_lo, 8) X(float, draw_hi, 8)                      \
+  X(int, param_draw, MAXP) /* reset source of each param: draw index / -1 default / -2 neck */  \
   /* depth renderer: every primitive geom (model order), its collidable index or -1 */        \
   X(int, rg_type, MAXRG) X(int, rg_body, MAXRG) X(int, rg_cgeom, MAXRG)                         \
   X(float, rg_pos, MAXRG * 3) X(float, rg_quat, MAXRG * 4) X(float, rg_size, MAXRG * 3)         \
@@ -161,12 +170,15 @@ struct DModel {
   int ntouch;
   int ndraw;              // reset uniform draws
   int task_kind, frame_skip, horizon, obs_dim, nparam, variation;
+  int success_steps;      // evaluate_success: an episode succeeds with > success_steps goal steps
   int iterations, noslip_iterations, mpr_iterations, disableflags;
   float timestep, gravity[3], tolerance, noslip_tolerance, mpr_tolerance, meaninertia;
   float pen_length, tar_length;
   int cls_start[NCLASS + 1];  // collider class c owns pair-list slots [cls_start[c], cls_start[c+1])
   int nrgeom;                 // rendered geoms
   const MData* __restrict__ d;
+  float* jspill;              // per-env dense-J overflow rows [nenv][JSPILL] (device)
+  unsigned long long env_offset;   // global id of env 0 of this handle (shards): Philox keys
 };
 
 // ---------------------------------------------------------------------------------------
@@ -222,9 +234,10 @@ struct __attribute__((aligned(16))) Env {
   signed char efc_i0[MAXEFC], efc_i1[MAXEFC];
   float efc_v0[MAXEFC], efc_v1[MAXEFC], efc_floss[MAXEFC], efc_D[MAXEFC];
   float efc_aref[MAXEFC], efc_force[MAXEFC];
-  float J[MAXDENSE][VS] __attribute__((aligned(16)));
+  float J[JL][VS] __attribute__((aligned(16)));
   float rowbuf[MAXEFC];
   unsigned status;
+  int env;                    // env index (selects the dense-J spill block)
   int it_newton, it_noslip;   // iterations of the last solve (introspection)
 #ifdef AW_STAGE_PROF
   unsigned long long prof_acc[AW_NPROF];

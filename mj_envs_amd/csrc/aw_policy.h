@@ -22,7 +22,7 @@ AW_DEV int mlp_param_count(int in, int h, int out) { return 2 * in + h * in + h 
 template <int H>
 __global__ void __launch_bounds__(256) k_mlp(int n, int in, int out, const float* __restrict__ p,
                                              const float* __restrict__ obs, float* __restrict__ act, int sample,
-                                             uint64_t seed, uint64_t step) {
+                                             uint64_t seed, uint64_t step, uint64_t env_offset) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   const float* in_shift = p;
@@ -60,10 +60,11 @@ __global__ void __launch_bounds__(256) k_mlp(int n, int in, int out, const float
 #pragma unroll
   for (int o = 0; o < MLP_OMAX; o++) nz[o] = 0.f;
   if (sample) {
-    // N(0, 1) by Box-Muller on Philox draws, counter = (env, step, 0x901C, block)
+    // N(0, 1) by Box-Muller on Philox draws, counter = (global env id, step, 0x901C, block)
 #pragma unroll
     for (int blk = 0; blk < MLP_OMAX / 4; blk++) {
-      uint32_t c[4] = {(uint32_t)e, (uint32_t)step, (uint32_t)(step >> 32) ^ 0x901Cu, (uint32_t)blk};
+      uint32_t c[4] = {(uint32_t)(env_offset + (uint64_t)e), (uint32_t)step, (uint32_t)(step >> 32) ^ 0x901Cu,
+                       (uint32_t)blk};
       philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
 #pragma unroll
       for (int q = 0; q < 2; q++) {

@@ -116,23 +116,48 @@ AW_DEV float getimpedance(const float* solimp, float pm) {
   return d0 + y * (dmax - d0);
 }
 
-// J_r . x  (x in LDS)
+// ---------------------------------------------------------------------------------------
+// Dense J storage: rows [0, JL) in LDS (s.J), rows [JL, ndense) in this env's global spill
+// block.  Spill rows are written and read with VECTOR memory instructions only: every read
+// below uses a lane-dependent address (a row per lane, or the row's entry per lane followed by
+// a readlane broadcast), so no uniform (scalar-cache) load can see a previous substep's row.
+AW_DEV float* jspill_row(const DModel& m, const Env& s, int d) {
+  return m.jspill + (size_t)s.env * JSPILL + (size_t)(d - JL) * VS;
+}
+AW_DEV void jput(const DModel& m, Env& s, int d, int k, float v) {
+  if (d < JL) s.J[d][k] = v;
+  else jspill_row(m, s, d)[k] = v;
+}
+// the wave's spill-row stores complete before any lane reads them back
+AW_DEV void jspill_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// J_r . x  (x in LDS); r is per lane
 template <int NV>
-AW_DEV float row_dot(const Env& s, int r, const float* x) {
+AW_DEV float row_dot(const DModel& m, const Env& s, int r, const float* x) {
   if (r < s.nsparse) {
     int i1 = s.efc_i1[r];
     return s.efc_v0[r] * x[s.efc_i0[r]] + (i1 >= 0 ? s.efc_v1[r] * x[i1] : 0.f);
   }
-  const float* J = s.J[r - s.nsparse];
+  const int d = r - s.nsparse;
   float acc = 0.f;
+  if (d < JL) {
+    const float* J = s.J[d];
 #pragma unroll
-  for (int k = 0; k < NV; k++) acc = fmaf(J[k], x[k], acc);
+    for (int k = 0; k < NV; k++) acc = fmaf(J[k], x[k], acc);
+  } else {
+    const float* J = jspill_row(m, s, d);
+#pragma unroll
+    for (int k = 0; k < NV; k++) acc = fmaf(J[k], x[k], acc);
+  }
   return acc;
 }
 
 // out_k = (J' f)_k for k = lane; f given per row in s.rowbuf (must be written + synced)
 template <int NV>
-AW_DEV float jt_mul(Env& s, int lane) {
+AW_DEV float jt_mul(const DModel& m, Env& s, int lane) {
   if (lane < NV) s.vec2[lane] = 0.f;
   wsync();
   for (int r = lane; r < s.nsparse; r += 64) {
@@ -146,7 +171,12 @@ AW_DEV float jt_mul(Env& s, int lane) {
   wsync();
   const int li = lane < NV ? lane : NV - 1;
   float out = s.vec2[li];
-  for (int d = 0; d < s.ndense; d++) out = fmaf(s.J[d][li], s.rowbuf[s.nsparse + d], out);
+  const int nd = s.ndense, ndl = nd < JL ? nd : JL;
+  for (int d = 0; d < ndl; d++) out = fmaf(s.J[d][li], s.rowbuf[s.nsparse + d], out);
+  if (nd > JL) {
+    const float* Jg = jspill_row(m, s, JL);
+    for (int d = JL; d < nd; d++, Jg += VS) out = fmaf(Jg[li], s.rowbuf[s.nsparse + d], out);
+  }
   return lane < NV ? out : 0.f;
 }
 
@@ -300,17 +330,18 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
       for (int q = 0; q < 3; q++) { B[q] = dot3(fr + 3 * q, jp); B[3 + q] = dot3(fr + 3 * q, jr); }
       int d = r0 - nsparse;
       if (cdim == 1) {
-        s.J[d][k] = B[0];
+        jput(m, s, d, k, B[0]);
       } else {
         for (int kk = 1; kk < cdim; kk++) {
           const float fri = kk == 1 ? rlane(c_f0, c) : (kk == 2 ? rlane(c_f1, c) : MD(cp_friction, 5 * pr + kk - 1));
-          s.J[d][k] = B[0] + fri * B[kk];
-          s.J[d + 1][k] = B[0] - fri * B[kk];
+          jput(m, s, d, k, B[0] + fri * B[kk]);
+          jput(m, s, d + 1, k, B[0] - fri * B[kk]);
           d += 2;
         }
       }
     }
   }
+  if (nd > JL) jspill_fence();
   wsync();
   // impedance, regularisation, reference acceleration
   for (int r = lane; r < s.nefc; r += 64) {
@@ -335,7 +366,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
     }
     float R = fmaxf((1.f - imp) * s.efc_force[r] / imp, MINVAL);
     s.efc_D[r] = 1.f / R;
-    float vel = row_dot<NV>(s, r, s.qvel);
+    float vel = row_dot<NV>(m, s, r, s.qvel);
     s.efc_aref[r] = -B * vel - K * imp * pm;
   }
   wsync();
@@ -368,8 +399,9 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
   const int nefc = s.nefc;
   const float fs = lane < NV ? qfrc_smooth : 0.f;
   const float a0 = lane < NV ? qacc_smooth : 0.f;
-  RowR rr[2];
-  for (int h = 0; h < 2; h++) {
+  RowR rr[NRL];
+#pragma unroll
+  for (int h = 0; h < NRL; h++) {
     int r = lane + 64 * h;
     rr[h].valid = r < nefc;
     int rc = rr[h].valid ? r : 0;
@@ -387,16 +419,18 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
     Ma = matvec<NV>(Mrow, a);
     if (lane < NV) s.vec[lane] = a;
     wsync();
-    for (int h = 0; h < 2; h++) {
+#pragma unroll
+    for (int h = 0; h < NRL; h++) {
       int r = lane + 64 * h;
-      if (r < nefc) rr[h].Jaref = row_dot<NV>(s, r, s.vec) - s.efc_aref[r];
+      if (r < nefc) rr[h].Jaref = row_dot<NV>(m, s, r, s.vec) - s.efc_aref[r];
     }
     wsync();
   };
   auto eval = [&]() {
     float g = lane < NV ? (Ma - fs) * (a - a0) : 0.f;
     float c = 0.f;
-    for (int h = 0; h < 2; h++) c += row_eval(rr[h], rr[h].Jaref, &rr[h].force, &rr[h].st);
+#pragma unroll
+    for (int h = 0; h < NRL; h++) c += row_eval(rr[h], rr[h].Jaref, &rr[h].force, &rr[h].st);
     return 0.5f * wave_sum(g) + wave_sum(c);
   };
   set_point(a0);
@@ -410,9 +444,10 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
   }
   float gref = 0.f;   // |Ma|^2 + |fs|^2 + |J'f|^2 per lane: the fp32 noise scale of the gradient
   auto gradient = [&]() {
-    for (int h = 0; h < 2; h++) { int r = lane + 64 * h; if (r < nefc) s.rowbuf[r] = rr[h].force; }
+#pragma unroll
+    for (int h = 0; h < NRL; h++) { int r = lane + 64 * h; if (r < nefc) s.rowbuf[r] = rr[h].force; }
     wsync();
-    float jf = jt_mul<NV>(s, lane);
+    float jf = jt_mul<NV>(m, s, lane);
     gref = lane < NV ? Ma * Ma + fs * fs + jf * jf : 0.f;
     return lane < NV ? Ma - fs - jf : 0.f;
   };
@@ -425,8 +460,9 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
     // couples; dense rows: rank-1 updates with the row broadcast from LDS.
     if (lane < NV) s.hdiag[lane] = 0.f;
     wsync();
-    unsigned long long offd[2];
-    for (int h = 0; h < 2; h++) {
+    unsigned long long offd[NRL];
+#pragma unroll
+    for (int h = 0; h < NRL; h++) {
       int r = lane + 64 * h;
       bool od = false;
       if (r < nefc) {
@@ -449,7 +485,8 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
 #pragma unroll
       for (int k = 0; k < NV; k++) H[k] = Mrow[k] + (k == lane ? dg : 0.f);
     }
-    for (int h = 0; h < 2; h++) {
+#pragma unroll
+    for (int h = 0; h < NRL; h++) {
       while (offd[h]) {
         const int r = 64 * h + __builtin_ctzll(offd[h]);
         offd[h] &= offd[h] - 1ull;
@@ -461,12 +498,25 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
         for (int k = 0; k < NV; k++) H[k] += k == other ? val : 0.f;
       }
     }
-    for (int d = 0; d < s.ndense; d++) {
+    const int nd = s.ndense, ndl = nd < JL ? nd : JL;
+    for (int d = 0; d < ndl; d++) {
       float w = s.rowbuf[s.nsparse + d];
       if (w == 0.f) continue;
       float av = w * s.J[d][li];
 #pragma unroll
       for (int k = 0; k < NV; k++) H[k] = fmaf(av, s.J[d][k], H[k]);
+    }
+    if (nd > JL) {
+      // spill rows: the row's entry per lane (coalesced), broadcast with readlane
+      const float* Jg = jspill_row(m, s, JL);
+      for (int d = JL; d < nd; d++, Jg += VS) {
+        float w = s.rowbuf[s.nsparse + d];
+        if (w == 0.f) continue;
+        const float jl = Jg[li];
+        const float av = w * jl;
+#pragma unroll
+        for (int k = 0; k < NV; k++) H[k] = fmaf(av, rlane(jl, k), H[k]);
+      }
     }
     wsync();
     AW_PROF(s, PR_NT_HESS);
@@ -483,14 +533,16 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
     float c1 = wave_sum(lane < NV ? p * Mp : 0.f);
     if (lane < NV) s.vec[lane] = p;
     wsync();
-    for (int h = 0; h < 2; h++) {
+#pragma unroll
+    for (int h = 0; h < NRL; h++) {
       int r = lane + 64 * h;
-      rr[h].Jp = r < nefc ? row_dot<NV>(s, r, s.vec) : 0.f;
+      rr[h].Jp = r < nefc ? row_dot<NV>(m, s, r, s.vec) : 0.f;
     }
     wsync();
     auto deriv = [&](float alpha, float* d1, float* d2) {
       float g1 = 0.f, g2 = 0.f;
-      for (int h = 0; h < 2; h++) {
+#pragma unroll
+      for (int h = 0; h < NRL; h++) {
         float jp = rr[h].Jp;
         if (!rr[h].valid || jp == 0.f) continue;
         float f;
@@ -521,7 +573,8 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
     if (alpha == 0.f) { iter++; break; }
     a += alpha * p;
     Ma += alpha * Mp;
-    for (int h = 0; h < 2; h++) rr[h].Jaref += alpha * rr[h].Jp;
+#pragma unroll
+    for (int h = 0; h < NRL; h++) rr[h].Jaref += alpha * rr[h].Jp;
     float oldcost = cost;
     cost = eval();
     grad = gradient();
@@ -538,7 +591,8 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
   AW_PROF_ADD(s, PR_NEWTON_IT, iter);
   AW_PROF_ADD(s, PR_NEFC, nefc);
   AW_PROF_ADD(s, PR_NCON, s.ncon);
-  for (int h = 0; h < 2; h++) {
+#pragma unroll
+  for (int h = 0; h < NRL; h++) {
     int r = lane + 64 * h;
     if (r < nefc) s.efc_force[r] = rr[h].force;
   }
@@ -611,7 +665,10 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
       fl_invA = 1.0f / dg;
     }
   }
+  // dense-row forces: row lane in fd, row 64 + lane in fd_hi (ndense <= MAXDENSE = 128)
+  float fd_hi = 0.f;
   if (lane < ndense) fd = s.efc_force[nsparse + lane];
+  if (lane + 64 < ndense) fd_hi = s.efc_force[nsparse + 64 + lane];
   qacc = lane < NV ? qacc : 0.f;
   const float scale = 1.f / (m.meaninertia * (float)(NV > 1 ? NV : 1));
   // opposing pyramid-edge pairs (e, e+1) in row order: x = inv(M) J_e' in registers, pair
@@ -622,14 +679,36 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
   float c_j1[NSP_CACHE], c_j2[NSP_CACHE], c_x1[NSP_CACHE], c_x2[NSP_CACHE];
 #pragma unroll
   for (int p = 0; p < NSP_CACHE; p++) c_j1[p] = c_j2[p] = c_x1[p] = c_x2[p] = 0.f;
-  auto edge_rows = [&](int e, float& j1, float& j2, float& x1, float& x2) {
-    j1 = lm * s.J[e][li];
-    j2 = lm * s.J[e + 1][li];
-    float a1 = 0.f, a2 = 0.f;
+  // J row d at this lane's dof, and (inv(M) J_d')_lane
+  auto jrow_x = [&](int d, float& jv, float& xv) {
+    float a = 0.f;
+    if (d < JL) {
+      jv = lm * s.J[d][li];
 #pragma unroll
-    for (int j = 0; j < NV; j++) { a1 = fmaf(Mi[j], s.J[e][j], a1); a2 = fmaf(Mi[j], s.J[e + 1][j], a2); }
-    x1 = a1; x2 = a2;
+      for (int j = 0; j < NV; j++) a = fmaf(Mi[j], s.J[d][j], a);
+    } else {
+      const float jl = jspill_row(m, s, d)[li];
+      jv = lm * jl;
+#pragma unroll
+      for (int j = 0; j < NV; j++) a = fmaf(Mi[j], rlane(jl, j), a);
+    }
+    xv = a;
   };
+  auto edge_rows = [&](int e, float& j1, float& j2, float& x1, float& x2) {
+    if (e + 1 < JL) {
+      j1 = lm * s.J[e][li];
+      j2 = lm * s.J[e + 1][li];
+      float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < NV; j++) { a1 = fmaf(Mi[j], s.J[e][j], a1); a2 = fmaf(Mi[j], s.J[e + 1][j], a2); }
+      x1 = a1; x2 = a2;
+    } else {
+      jrow_x(e, j1, x1);
+      jrow_x(e + 1, j2, x2);
+    }
+  };
+  // dense-row force of row e (uniform) / its update
+  auto fd_get = [&](int e) { return e < 64 ? rlane(fd, e) : rlane(fd_hi, e - 64); };
   for (int e = 0; e + 1 < ndense; e++) {
     if (!(s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1)) continue;
     float j1, j2, x1, x2;
@@ -676,7 +755,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
       const float A11 = rlane(pr_a11, p), A22 = rlane(pr_a22, p), A12 = rlane(pr_a12, p);
       const float r1 = wave_sum(j1 * qacc) - rlane(pr_ar1, p);
       const float r2 = wave_sum(j2 * qacc) - rlane(pr_ar2, p);
-      const float f1 = rlane(fd, e), f2 = rlane(fd, e + 1);
+      const float f1 = fd_get(e), f2 = fd_get(e + 1);
       const float sum = f1 + f2, x = f1 - f2;
       const float xn = clampf(x - 2.f * (r1 - r2) * rlane(pr_ik, p), -sum, sum);
       const float d1 = 0.5f * (sum + xn) - f1, d2 = 0.5f * (sum - xn) - f2;
@@ -684,6 +763,8 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
       qacc = fmaf(x1, d1, fmaf(x2, d2, qacc));
       if (lane == e) fd = f1 + d1;
       if (lane == e + 1) fd = f2 + d2;
+      if (lane + 64 == e) fd_hi = f1 + d1;
+      if (lane + 64 == e + 1) fd_hi = f2 + d2;
     };
 #pragma unroll
     for (int p = 0; p < NSP_CACHE; p++)
@@ -698,6 +779,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
   AW_PROF(s, PR_NS_ITER);
   if (lane < NV && MD(fl_row, lane) >= 0 && MD(fl_row, lane) < nsparse) s.efc_force[MD(fl_row, lane)] = ffl;
   if (lane < ndense) s.efc_force[nsparse + lane] = fd;
+  if (lane + 64 < ndense) s.efc_force[nsparse + 64 + lane] = fd_hi;
   wsync();
 }
 

@@ -215,7 +215,7 @@ AW_DEV void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
 }
 AW_DEV float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
 
-// reset draws -> params (tasks.draws_to_params); counter = (env, episode, stream 0x5EED, block)
+// reset draws -> params (tasks.draws_to_params); counter = (global env id, episode, stream 0x5EED, block)
 AW_DEV void sample_params(const DModel& m, uint64_t seed, uint32_t genv, uint32_t episode, float* params) {
   float u[8];
 #pragma unroll
@@ -230,14 +230,19 @@ AW_DEV void sample_params(const DModel& m, uint64_t seed, uint32_t genv, uint32_
   if (m.task_kind == 2) {
     float eu[3] = {d[0], d[1], 0.f};
     euler2quat_ref(eu, params);
-  } else if (m.task_kind == 0 && m.variation == 2) {
-    params[0] = d[0];
-    params[1] = d[1];
-    params[2] = -0.14f - (-0.24f - d[1]);
-  } else {
+    return;
+  }
+  // tasks.param_draws: draw index, -1 keep (a field reset_model does not write keeps its last
+  // value: the reference's model mutations persist across resets), -2 hammer
+  // 'pos' neck x (hammer_v0.py:122).  params holds the env's current values on entry.
 #pragma unroll
-    for (int k = 0; k < MAXP; k++)
-      if (k < m.nparam) params[k] = d[k];
+  for (int p = 0; p < MAXP; p++) {
+    if (p >= m.nparam) break;
+    const int c = MD(param_draw, p);
+    float v = c == -2 ? -0.14f - (-0.24f - d[1]) : params[p];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v = c == k ? d[k] : v;
+    params[p] = v;
   }
 }
 

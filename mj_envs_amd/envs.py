@@ -22,7 +22,7 @@ from typing import Dict, List, Optional
 import numpy as np
 
 from . import _native
-from .tasks import TASKS, attach_task, load_model, param_layout
+from .tasks import TASKS, attach_task, env_state_from, env_state_to_params, load_model, param_layout
 
 
 class Box:
@@ -78,6 +78,7 @@ class AdroitVecEnv:
         self.done = s.empty(num_envs, dtype=torch.uint8)
         self.goal = s.empty(num_envs, dtype=torch.uint8)
         self.terminal_obs = s.empty(num_envs, self.obs_dim)
+        self._status = s.empty(num_envs, dtype=torch.int32)
         self._resets = 0
 
     # --- episode control -------------------------------------------------------------------
@@ -96,7 +97,9 @@ class AdroitVecEnv:
                       autoreset=self.autoreset, seed=self.seed)
         terminated = (self.done & 1).bool()
         truncated = (self.done & 2).bool()
-        info = {"goal_achieved": self.goal.bool(), "terminal_obs": self.terminal_obs}
+        self.sim.status(last=self._status)
+        info = {"goal_achieved": self.goal.bool(), "terminal_obs": self.terminal_obs,
+                "status": self._status}    # AW_ST_* flags of this step (NaN reset, overflow)
         return self.obs, self.reward, terminated, truncated, info
 
     def random_actions(self, out, step: int, seed: int = 0):
@@ -136,10 +139,20 @@ class AdroitVecEnv:
         s.episode_stats(out["last_return"], out["last_goal_steps"], out["last_len"], out["episodes"])
         return out
 
-    def status(self):
+    def status(self, sticky: bool = False):
+        """AW_ST_* flags per env: of the last step, or (sticky) OR'ed since creation"""
         import torch
         out = self.sim.empty(self.num_envs, dtype=torch.int32)
-        self.sim.status(out)
+        self.sim.status(**({"sticky": out} if sticky else {"last": out}))
+        return out
+
+    def episode_totals(self):
+        """every finished episode counted once: episodes, sum of returns, successes per env"""
+        import torch
+        s = self.sim
+        out = dict(episodes=s.empty(self.num_envs, dtype=torch.int32), sum_return=s.empty(self.num_envs),
+                   successes=s.empty(self.num_envs, dtype=torch.int32))
+        s.episode_totals(out["episodes"], out["sum_return"], out["successes"])
         return out
 
     def evaluate_success(self, paths: List[dict]) -> float:
@@ -209,6 +222,24 @@ class _AdroitEnv:
     def _params(self) -> np.ndarray:
         return self.vec.get_state()["params"][0].cpu().numpy().astype(np.float64)
 
+    def get_env_state(self):
+        """``get_env_state`` of the reference task (hammer_v0.py:134-143, door_v0.py:121-128,
+        pen_v0.py:134-141, relocate_v0.py:105-116): same keys, fp64 copies."""
+        qp, qv = self._qpos_qvel()
+        xpos = site_xpos = None
+        if self.env_id == "hammer-v0":
+            site_xpos = {int(self.model.arrays["task_idx"][3]): self._obs[42:45]}   # last forward's S_target
+        elif self.env_id == "relocate-v0":
+            d = self.vec.sim.forward_dump(0)
+            xpos, site_xpos = d["xpos"], d["site_xpos"]
+        return env_state_from(self.env_id, self.model, qp, qv, self._params(), xpos=xpos, site_xpos=site_xpos)
+
+    def set_env_state(self, state_dict):
+        """``set_env_state``: qpos / qvel, then the whole model-field vectors the reference writes
+        (hammer board_pos, door frame body_pos, pen target quat, relocate obj / target pos)."""
+        p = env_state_to_params(self.env_id, state_dict, self._params())
+        self._set(state_dict["qpos"], state_dict["qvel"], p)
+
     def _set(self, qpos, qvel, params):
         import torch
         t = lambda x: torch.as_tensor(np.asarray(x, np.float32).reshape(1, -1), device=self._dev)
@@ -236,60 +267,24 @@ class HammerEnvV0(_AdroitEnv):
     """``hand_manipulation_suite/hammer_v0.py`` (obs 46, frame_skip 5, horizon 200)."""
     env_id = "hammer-v0"
 
-    def get_env_state(self):   # hammer_v0.py:134-143
-        qp, qv = self._qpos_qvel()
-        board = self.model.body_pos[self._layout[0][1]].astype(np.float64).copy()
-        board[2] = self._params()[0]
-        return dict(qpos=qp, qvel=qv, board_pos=board, target_pos=self._obs[42:45].astype(np.float64))
-
-    def set_env_state(self, state_dict):   # hammer_v0.py:145-153
-        p = self._params()
-        p[0] = np.asarray(state_dict["board_pos"])[2]
-        self._set(state_dict["qpos"], state_dict["qvel"], p)
-
 
 class DoorEnvV0(_AdroitEnv):
     """``hand_manipulation_suite/door_v0.py`` (obs 39, frame_skip 1, horizon 200)."""
     env_id = "door-v0"
-
-    def get_env_state(self):   # door_v0.py:121-128
-        qp, qv = self._qpos_qvel()
-        return dict(qpos=qp, qvel=qv, door_body_pos=self._params()[:3])
-
-    def set_env_state(self, state_dict):   # door_v0.py:130-138
-        self._set(state_dict["qpos"], state_dict["qvel"], np.asarray(state_dict["door_body_pos"])[:3])
 
 
 class PenEnvV0(_AdroitEnv):
     """``hand_manipulation_suite/pen_v0.py`` (obs 45, frame_skip 5, horizon 100, done on drop)."""
     env_id = "pen-v0"
 
-    def get_env_state(self):   # pen_v0.py:134-141
-        qp, qv = self._qpos_qvel()
-        return dict(qpos=qp, qvel=qv, desired_orien=self._params()[:4])
-
-    def set_env_state(self, state_dict):   # pen_v0.py:143-152
-        self._set(state_dict["qpos"], state_dict["qvel"], np.asarray(state_dict["desired_orien"])[:4])
-
 
 class RelocateEnvV0(_AdroitEnv):
     """``hand_manipulation_suite/relocate_v0.py`` (obs 39, frame_skip 5, horizon 200).
 
     ``get_env_state`` takes object / palm / target positions from a fresh forward pass of the
-    current state (the reference reads the previous forward's values; after ``reset`` or
-    ``set_env_state`` they coincide).  ``set_env_state`` writes the object's body x/y (the
-    reset-randomised components) and the target site position, as ``relocate_v0.py:118-129``.
+    current state (the reference reads the previous forward's values, and returns live views of
+    them; after ``reset`` or ``set_env_state`` they coincide).  ``set_env_state`` writes all of
+    ``obj_pos`` -- the object's body_xpos, joint displacement included -- into the object's
+    body_pos, and ``target_pos`` into the target site, as ``relocate_v0.py:118-129`` does.
     """
     env_id = "relocate-v0"
-
-    def get_env_state(self):   # relocate_v0.py:105-116
-        qp, qv = self._qpos_qvel()
-        d = self.vec.sim.forward_dump(0)
-        idx = self.model.arrays["task_idx"]
-        return dict(hand_qpos=qp[:30], obj_pos=d["xpos"][idx[1]].copy(), target_pos=d["site_xpos"][idx[2]].copy(),
-                    palm_pos=d["site_xpos"][idx[0]].copy(), qpos=qp, qvel=qv)
-
-    def set_env_state(self, state_dict):   # relocate_v0.py:118-129
-        obj = np.asarray(state_dict["obj_pos"])
-        tgt = np.asarray(state_dict["target_pos"])
-        self._set(state_dict["qpos"], state_dict["qvel"], np.array([obj[0], obj[1], tgt[0], tgt[1], tgt[2]]))

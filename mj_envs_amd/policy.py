@@ -10,9 +10,10 @@ applied with ``torch.manual_seed``, layers take torch's ``nn.Linear`` default in
 layer's weight and bias are scaled by 1e-2.
 
 The forward pass runs in the HIP kernel ``k_mlp`` (``aw_policy_mlp``, one thread per env).
-The reference's pretrained DAPG policies are pickles (``algos/dapg_pretrained/*.pickle``),
-which are never unpickled here, so this module covers the architecture and its random
-initialisation (the reference's ``is_random`` path), not those weights.
+``GaussianMLP.from_npz`` loads the reference's pretrained DAPG policies
+(``algos/dapg_pretrained/*.pickle``) from the inert fixtures ``tests/golden/dapg_<task>.npz``
+that ``tests/golden/make_dapg.py`` extracted WITHOUT unpickling (opcode-level data walk, tensors
+through ``torch.load(weights_only=True)``): hammer / door / relocate 32x32, pen 64x64.
 """
 from __future__ import annotations
 
@@ -50,6 +51,34 @@ class GaussianMLP:
         self._dev = None
         self.upload()
 
+    @classmethod
+    def from_npz(cls, path: str, device: int = 0) -> "GaussianMLP":
+        """Pretrained weights (``W0 b0 W1 b1 W2 b2`` in nn.Linear [out, in] layout, ``in_shift
+        in_scale out_shift out_scale log_std``), e.g. tests/golden/dapg_hammer.npz."""
+        d = np.load(path, allow_pickle=False)
+        sizes = tuple(int(x) for x in d["layer_sizes"])
+        self = cls.__new__(cls)
+        self.obs_dim, self.act_dim = sizes[0], sizes[-1]
+        hs = sizes[1:-1]
+        if len(hs) != 2 or hs[0] != hs[1] or hs[0] not in (32, 64):
+            raise ValueError(f"aw_policy_mlp supports two equal hidden layers of width 32 or 64, got {hs}")
+        self.hidden = hs[0]
+        self.weights = [(np.asarray(d[f"W{i}"], np.float64), np.asarray(d[f"b{i}"], np.float64)) for i in range(3)]
+        for k in ("in_shift", "in_scale", "out_shift", "out_scale", "log_std"):
+            setattr(self, k, np.asarray(d[k], np.float64))
+        self.device = device
+        self._dev = None
+        self.upload()
+        return self
+
+    def mean_np(self, obs: np.ndarray) -> np.ndarray:
+        """fp64 host forward of the mean (mjrl FCNetwork.forward), for checks."""
+        (W0, b0), (W1, b1), (W2, b2) = self.weights
+        x = (np.asarray(obs, np.float64) - self.in_shift) / (self.in_scale + 1e-8)
+        x = np.tanh(x @ W0.T + b0)
+        x = np.tanh(x @ W1.T + b1)
+        return (x @ W2.T + b2) * self.out_scale + self.out_shift
+
     def flat_params(self) -> np.ndarray:
         """Parameter block in the aw_policy_mlp layout (aw_policy.h)."""
         (W0, b0), (W1, b1), (W2, b2) = self.weights
@@ -61,9 +90,9 @@ class GaussianMLP:
         import torch
         self._dev = torch.tensor(self.flat_params(), device=torch.device("cuda", self.device))
 
-    def act(self, obs, out=None, sample: bool = False, seed: int = 0, step: int = 0):
+    def act(self, obs, out=None, sample: bool = False, seed: int = 0, step: int = 0, env_offset: int = 0):
         """actions [n, act_dim] (device) from obs [n, obs_dim] (device fp32): the mean, or with
-        sample=True mean + exp(log_std) * N(0, 1) from Philox (seed, (env, step))."""
+        sample=True mean + exp(log_std) * N(0, 1) from Philox (seed, (env_offset + env, step))."""
         import torch
         n = obs.shape[0]
         assert obs.shape[1] == self.obs_dim and obs.is_contiguous() and obs.dtype == torch.float32
@@ -72,5 +101,5 @@ class GaussianMLP:
         L = _native.load()
         _native._check(L.aw_policy_mlp(n, self.obs_dim, self.hidden, self.act_dim, self._dev.data_ptr(),
                                        obs.data_ptr(), out.data_ptr(), int(sample), ctypes.c_uint64(seed),
-                                       ctypes.c_uint64(step), _native._stream()))
+                                       ctypes.c_uint64(step), ctypes.c_uint64(env_offset), _native._stream()))
         return out

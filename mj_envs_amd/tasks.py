@@ -76,7 +76,10 @@ def param_layout(env_id: str, model, variation_type: Optional[str] = None) -> Li
     """(field, object id, component) for every per-env parameter, in params[] order."""
     n = model.name2id
     if env_id == "hammer-v0":
-        lay = [("body_pos", n("body", "nail_board"), 2)]
+        # the whole nail-board position: set_env_state writes all of board_pos (hammer_v0.py:152);
+        # reset draws only z (:109)
+        board = n("body", "nail_board")
+        lay = [("body_pos", board, 0), ("body_pos", board, 1), ("body_pos", board, 2)]
         head, neck = n("geom", "head"), n("geom", "neck")
         if variation_type == "mass":
             lay.append(("body_mass", n("body", "Object"), 0))
@@ -94,9 +97,31 @@ def param_layout(env_id: str, model, variation_type: Optional[str] = None) -> Li
         b = n("body", "target")
         return [("body_quat", b, k) for k in range(4)]
     if env_id == "relocate-v0":
+        # object body_pos (all three: set_env_state writes obj_pos, relocate_v0.py:127) and the
+        # target site; reset draws object x / y and target x / y / z (:89-93)
         b, s = n("body", "Object"), n("site", "target")
-        return [("body_pos", b, 0), ("body_pos", b, 1),
+        return [("body_pos", b, 0), ("body_pos", b, 1), ("body_pos", b, 2),
                 ("site_pos", s, 0), ("site_pos", s, 1), ("site_pos", s, 2)]
+    raise KeyError(env_id)
+
+
+# source of each param at a reset: the index of a uniform draw (reset_ranges order), or
+# PD_DEFAULT (keeps its current value -- the model value for a fresh env: a field reset_model does
+# not write keeps what was last written), PD_NECK (hammer 'pos' variation: neck x = -0.14 - (-0.24 - x),
+# hammer_v0.py:122), PD_QUAT (pen: euler2quat of draws 0 / 1, pen_v0.py:119-122)
+PD_DEFAULT, PD_NECK, PD_QUAT = -1, -2, -3
+
+
+def param_draws(env_id: str, variation_type: Optional[str] = None) -> List[int]:
+    if env_id == "hammer-v0":
+        return [PD_DEFAULT, PD_DEFAULT, 0] + {None: [], "mass": [1], "pos": [1, PD_NECK],
+                                              "size": [1, 2]}[variation_type]
+    if env_id == "door-v0":
+        return [0, 1, 2]
+    if env_id == "pen-v0":
+        return [PD_QUAT] * 4
+    if env_id == "relocate-v0":
+        return [0, 1, PD_DEFAULT, 2, 3, 4]
     raise KeyError(env_id)
 
 
@@ -136,17 +161,27 @@ def euler2quat(euler):
     return quat
 
 
-def draws_to_params(env_id: str, u: np.ndarray, variation_type: Optional[str] = None) -> np.ndarray:
-    """Map uniform draws (already scaled to reset_ranges) to the override vector."""
+def draws_to_params(env_id: str, u: np.ndarray, variation_type: Optional[str] = None,
+                    defaults: Optional[np.ndarray] = None) -> np.ndarray:
+    """Map uniform draws (already scaled to reset_ranges) to the override vector
+    (``param_draws``); ``defaults``: the current params (``default_params`` for a fresh env)."""
     u = np.atleast_2d(np.asarray(u, np.float64))
     if env_id == "pen-v0":
         e = np.zeros((u.shape[0], 3))
         e[:, 0], e[:, 1] = u[:, 0], u[:, 1]
         return euler2quat(e)
-    if env_id == "hammer-v0" and variation_type == "pos":
-        x = u[:, 1]
-        return np.stack([u[:, 0], x, -0.14 - (-0.24 - x)], axis=1)
-    return u.copy()
+    codes = param_draws(env_id, variation_type)
+    out = np.zeros((u.shape[0], len(codes)))
+    for p, c in enumerate(codes):
+        if c >= 0:
+            out[:, p] = u[:, c]
+        elif c == PD_NECK:
+            out[:, p] = -0.14 - (-0.24 - u[:, 1])
+        else:
+            if defaults is None:
+                raise ValueError("draws_to_params: defaults needed for params kept at the model value")
+            out[:, p] = defaults[p]
+    return out
 
 
 def default_params(env_id: str, model, variation_type: Optional[str] = None) -> np.ndarray:
@@ -166,7 +201,7 @@ def sample_params(env_id: str, model, rng: np.random.Generator, n: int,
     for i in range(n):
         for k, (lo, hi) in enumerate(ranges):
             u[i, k] = rng.uniform(low=lo, high=hi)
-    return draws_to_params(env_id, u, variation_type)
+    return draws_to_params(env_id, u, variation_type, default_params(env_id, model, variation_type))
 
 
 # ---------------------------------------------------------------------------------------
@@ -212,13 +247,14 @@ def attach_task(model, env_id: str, variation_type: Optional[str] = None):
     m.arrays["task_param_obj"] = np.array([o for _, o, _ in lay], np.int32)
     m.arrays["task_param_comp"] = np.array([c for _, _, c in lay], np.int32)
     m.arrays["task_param_default"] = default_params(env_id, model, variation_type)
+    m.arrays["task_param_draw"] = np.array(param_draws(env_id, variation_type), np.int32)
     rr = reset_ranges(env_id, variation_type)
     m.arrays["task_draw_lo"] = np.array([r[0] for r in rr])
     m.arrays["task_draw_hi"] = np.array([r[1] for r in rr])
     var = {None: 0, "mass": 1, "pos": 2, "size": 3}[variation_type]
     m.dims.update(task_kind=spec.kind, task_frame_skip=spec.frame_skip, task_horizon=spec.horizon,
                   task_obs_dim=spec.obs_dim, task_nparam=len(lay), task_variation=var,
-                  task_mpr_fp64=int(spec.mpr_fp64))
+                  task_mpr_fp64=int(spec.mpr_fp64), task_success_steps=spec.success_steps)
     if env_id == "pen-v0":
         pl, tl = pen_lengths(model)
         m.opt.update(task_pen_length=pl, task_tar_length=tl)
@@ -227,3 +263,47 @@ def attach_task(model, env_id: str, variation_type: Optional[str] = None):
     m.arrays["task_act_mid"] = np.mean(cr, axis=1)
     m.arrays["task_act_rng"] = 0.5 * (cr[:, 1] - cr[:, 0])
     return m
+
+
+# ---------------------------------------------------------------------------------------
+# get_env_state / set_env_state dicts <-> per-env params (hammer_v0.py:134-153,
+# door_v0.py:121-138, pen_v0.py:134-152, relocate_v0.py:105-129)
+def env_state_to_params(env_id: str, state: dict, params: np.ndarray) -> np.ndarray:
+    """params after ``set_env_state(state)`` of an env whose params were ``params``: the model
+    fields the reference writes, whole vectors (variation params are left as they are)."""
+    p = np.array(params, np.float64, copy=True)
+    if env_id == "hammer-v0":
+        p[0:3] = np.asarray(state["board_pos"], np.float64).ravel()[:3]
+    elif env_id == "door-v0":
+        p[0:3] = np.asarray(state["door_body_pos"], np.float64).ravel()[:3]
+    elif env_id == "pen-v0":
+        p[0:4] = np.asarray(state["desired_orien"], np.float64).ravel()[:4]
+    elif env_id == "relocate-v0":
+        # obj_pos is the object's body_xpos (joint displacement included) written into body_pos:
+        # the reference's quirk is kept (relocate_v0.py:127)
+        p[0:3] = np.asarray(state["obj_pos"], np.float64).ravel()[:3]
+        p[3:6] = np.asarray(state["target_pos"], np.float64).ravel()[:3]
+    else:
+        raise KeyError(env_id)
+    return p
+
+
+def env_state_from(env_id: str, model, qpos, qvel, params, xpos=None, site_xpos=None) -> dict:
+    """The reference's get_env_state dict from the state, the params and (hammer target_pos,
+    relocate obj / palm / target) the kinematics of the last forward pass."""
+    qpos = np.asarray(qpos, np.float64).copy()
+    qvel = np.asarray(qvel, np.float64).copy()
+    p = np.asarray(params, np.float64)
+    idx = task_indices(env_id, model)
+    if env_id == "hammer-v0":
+        return dict(qpos=qpos, qvel=qvel, board_pos=p[0:3].copy(),
+                    target_pos=np.asarray(site_xpos[idx[3]], np.float64).copy())
+    if env_id == "door-v0":
+        return dict(qpos=qpos, qvel=qvel, door_body_pos=p[0:3].copy())
+    if env_id == "pen-v0":
+        return dict(qpos=qpos, qvel=qvel, desired_orien=p[0:4].copy())
+    if env_id == "relocate-v0":
+        return dict(hand_qpos=qpos[:30].copy(), obj_pos=np.asarray(xpos[idx[1]], np.float64).copy(),
+                    target_pos=np.asarray(site_xpos[idx[2]], np.float64).copy(),
+                    palm_pos=np.asarray(site_xpos[idx[0]], np.float64).copy(), qpos=qpos, qvel=qvel)
+    raise KeyError(env_id)

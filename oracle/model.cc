@@ -70,8 +70,8 @@ int load_model(Model* m, const void* blob, size_t nbytes) {
   m->mpr_iterations = (int)aw_blob_opt(blob, nbytes, "mpr_iterations", 50);
   m->meaninertia = aw_blob_opt(blob, nbytes, "meaninertia", 1);
   m->disableflags = 0;
-  m->max_con = 64;
-  m->max_efc = 512;
+  m->max_con = 100;   // MuJoCo's nconmax / njmax of the reference model (DAPG_assets.xml:4)
+  m->max_efc = 500;
 
   r.i("body_parentid", m->body_parentid); r.i("body_rootid", m->body_rootid);
   r.i("body_weldid", m->body_weldid); r.i("body_jntnum", m->body_jntnum);

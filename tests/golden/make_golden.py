@@ -12,7 +12,7 @@ them.  ``do_simulation`` is stubbed to record the ctrl it receives (checks the a
 clip/scale of hammer_v0.py:55-59) and to leave the synthetic mjData in place.
 
 Outputs (data only, no reference source): tests/golden/task_<env>.npz, quatmath.npz,
-reset_<env>[_<variation>].npz.
+reset_<env>[_<variation>].npz, state_<env>.npz (get_env_state / set_env_state semantics).
 """
 import importlib
 import os
@@ -274,6 +274,42 @@ def gen_reset(env_id, cls_name, module, variation=None, n=16, seed=777):
     print("reset", tag, np.array(vals)[:2])
 
 
+def gen_state(env_id, cls_name, module, n=8, seed=99):
+    """get_env_state -> set_env_state semantics: on a synthetic mid-episode mjData (object moved
+    off its body_pos, so body_xpos != body_pos), record the reference's get_env_state dict and
+    the model fields / state its set_env_state writes on a fresh env (data only)."""
+    from mj_envs_amd.tasks import load_model, param_layout
+    model = load_model(env_id)
+    lay = param_layout(env_id, model, None)
+    rng = np.random.default_rng(seed)
+    rec = {}
+    for i in range(n):
+        env = make_env(module, cls_name, env_id, model)
+        env.variation_type = None
+        env.np_random = np.random.default_rng(seed + i)
+        env.reset_model()
+        d = env.data
+        d.qpos[:] = rng.uniform(-1, 1, model.nq)
+        d.qvel[:] = rng.normal(size=model.nv)
+        d.body_xpos[:] = rng.uniform(-0.5, 0.5, (model.nbody, 3))
+        d.site_xpos[:] = rng.uniform(-0.5, 0.5, (model.nsite, 3))
+        got = {k: np.array(v, np.float64).copy() for k, v in env.get_env_state().items()}
+        fresh = make_env(module, cls_name, env_id, model)
+        fresh.set_env_state({k: v.copy() for k, v in got.items()})
+        after = [getattr(fresh.model, f)[o] if getattr(fresh.model, f).ndim == 1 else getattr(fresh.model, f)[o, c]
+                 for f, o, c in lay]
+        row = {f"get_{k}": v for k, v in got.items()}
+        row.update(params_after=np.array(after), qpos_after=fresh.data.qpos.copy(), qvel_after=fresh.data.qvel.copy(),
+                   xpos=d.body_xpos.copy(), site_xpos=d.site_xpos.copy(), qpos=d.qpos.copy(), qvel=d.qvel.copy(),
+                   params_before=np.array([getattr(env.model, f)[o] if getattr(env.model, f).ndim == 1
+                                           else getattr(env.model, f)[o, c] for f, o, c in lay]))
+        for k, v in row.items():
+            rec.setdefault(k, []).append(v)
+    out = {k: np.array(v) for k, v in rec.items()}
+    np.savez_compressed(os.path.join(OUT, f"state_{env_id.split('-')[0]}.npz"), **out)
+    print("state", env_id, sorted(out))
+
+
 def gen_quatmath():
     sys.path.insert(0, os.path.join(REF, "mj_envs_vision", "utils"))
     qm = importlib.import_module("quatmath")
@@ -304,6 +340,7 @@ def main():
     for e in mods:
         gen_task(e, names[e], mods[e])
         gen_reset(e, names[e], mods[e])
+        gen_state(e, names[e], mods[e])
     for v in ("mass", "pos", "size"):
         gen_reset("hammer-v0", "HammerEnvV0", mods["hammer-v0"], variation=v)
 

@@ -63,8 +63,7 @@ def test_task_layer_golden(env_id):
 def contact_states(env_id, n, steps, seed=0):
     """Oracle rollouts with random actions -> (params, qpos, qvel, warm) with contacts."""
     from mj_envs_amd.tasks import sample_params
-    m, o = make_oracle(env_id)
-    o.set_option(max_con=32, max_efc=128)
+    m, o = make_oracle(env_id)           # MuJoCo's capacities: nconmax 100 / njmax 500
     rng = np.random.default_rng(seed)
     P = sample_params(env_id, m, rng, n)
     st, _ = o.reset(P)
@@ -76,6 +75,36 @@ def contact_states(env_id, n, steps, seed=0):
 def rel(a, b):
     a, b = np.asarray(a, float), np.asarray(b, float)
     return np.abs(a - b).max() / (np.abs(b).max() + 1e-9)
+
+
+# Pass fractions (per env or per (env, step) case) of the one-step state tolerance.  The
+# remainder are discrete events: a contact within fp32 rounding of the margin, or a bonus
+# threshold, switching in one precision and not the other.
+ONE_STEP_MIN = 0.97
+VARIATION_MIN = 0.97
+REWARD_MIN = 0.995
+
+
+def _no_overflow(sim, n):
+    """the kernel's capacities held: no env raised a contact / constraint overflow (sticky flags)"""
+    from mj_envs_amd import _native
+    st = sim.empty(n, dtype=torch.int32)
+    sim.status(sticky=st)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    assert not (st & _native.ST_OVERFLOW).any(), f"{int(((st & _native.ST_OVERFLOW) != 0).sum())} envs overflowed"
+
+
+def _rewards_close(r, r_ref, check=True):
+    """rewards of ALL envs: within 1e-3 (+1e-3 relative) or, where a bonus threshold flipped
+    between the precisions, off by exactly a bonus of the task (2, 8, 10, 20, 25, 50, 75 and sums)"""
+    d = np.abs(np.asarray(r, float) - np.asarray(r_ref, float))
+    tol = 1e-3 + 1e-3 * np.abs(r_ref)
+    ok = d <= tol
+    if check:
+        frac = ok.mean()
+        assert frac >= REWARD_MIN, (frac, np.where(~ok)[0], d[~ok])
+    return ok
 
 
 @pytest.mark.parametrize("env_id", ENVS)
@@ -122,8 +151,10 @@ def test_one_env_step_from_identical_states(env_id):
     okq = (np.abs(q - st["qpos"]) <= 2e-5 + 1e-5 * np.abs(st["qpos"])).all(axis=1)
     okv = (np.abs(v - st["qvel"]) <= 5e-3 * (1 + np.abs(st["qvel"]))).all(axis=1)
     ok = okq & okv
-    assert ok.mean() >= 0.95, (env_id, np.where(~ok)[0])
-    np.testing.assert_allclose(rew.cpu().numpy()[ok], r_ref[ok], rtol=1e-3, atol=1e-3)
+    print(f"one-step {env_id}: {ok.mean():.4f} of {n} envs within tolerance")
+    assert ok.mean() >= ONE_STEP_MIN, (env_id, np.where(~ok)[0])
+    _no_overflow(sim, n)
+    _rewards_close(rew.cpu().numpy(), r_ref)
 
 
 def test_smooth_dynamics_tight():
@@ -257,6 +288,14 @@ def test_teacher_forced_trajectory(env_id):
     assert frac >= TEACHER_FORCED_MIN[env_id], (env_id, frac)
 
 
+@pytest.mark.parametrize("env_id", ENVS)
+def test_teacher_forced_dapg_grasp(env_id):
+    """Teacher forcing along DAPG-policy rollouts (grasp / manipulation regime: up to ~20
+    contacts and ~100 dense rows per substep), oracle at MuJoCo's capacities, no overflow."""
+    frac = _teacher_forced(env_id, 0, policy=True, steps=80)
+    assert frac >= TEACHER_FORCED_MIN[env_id], (env_id, frac)
+
+
 @pytest.mark.parametrize("env_id", sorted(TEACHER_FORCED_MIN_MPR_OTHER))
 def test_teacher_forced_trajectory_other_mpr_precision(env_id):
     from mj_envs_amd._native import DSBL_MPR_FP32, DSBL_MPR_FP64
@@ -265,7 +304,7 @@ def test_teacher_forced_trajectory_other_mpr_precision(env_id):
     assert frac >= TEACHER_FORCED_MIN_MPR_OTHER[env_id], (env_id, frac)
 
 
-def _teacher_forced(env_id, disableflags):
+def _teacher_forced(env_id, disableflags, policy=False, steps=40):
     """SURVEY §8d C3 (multi-task correctness vs the CPU path): along a 40-step GPU rollout of
     64 envs, every env-step is re-run by the fp64 oracle from the GPU's own pre-step state
     (qpos, qvel, warmstart, params) with the same action; the GPU's post-step state must match
@@ -273,9 +312,8 @@ def _teacher_forced(env_id, disableflags):
     keeps the comparison per-step: free-running fp32 vs fp64 contact trajectories diverge
     (chaos), which says nothing about either.  Thresholds: TEACHER_FORCED_MIN."""
     from mj_envs_amd.tasks import sample_params
-    n, steps = 64, 40
+    n = 64
     m, o = make_oracle(env_id)
-    o.set_option(max_con=32, max_efc=128)
     _, sim = _sim(env_id, n)
     sim.set_option(disableflags=disableflags)
     P = sample_params(env_id, m, np.random.default_rng(11), n)
@@ -285,28 +323,38 @@ def _teacher_forced(env_id, disableflags):
     done, goal = sim.empty(n, dtype=torch.uint8), sim.empty(n, dtype=torch.uint8)
     q, v, w = sim.empty(n, sim.nq), sim.empty(n, sim.nv), sim.empty(n, sim.nv)
     rng = np.random.default_rng(13)
+    pol = None
+    if policy:
+        import os
+        from conftest import GOLDEN
+        from mj_envs_amd.policy import GaussianMLP
+        pol = GaussianMLP.from_npz(os.path.join(GOLDEN, f"dapg_{env_id.split('-')[0]}.npz"))
     oks, rok = [], []
+    ostatus = 0
     for k in range(steps):
         sim.get_state(q, v, w)
         torch.cuda.synchronize()
         st = dict(qpos=q.cpu().numpy().astype(np.float64), qvel=v.cpu().numpy().astype(np.float64),
                   warm=w.cpu().numpy().astype(np.float64), params=np.asarray(P, np.float64))
-        act = rng.uniform(-1, 1, (n, sim.nu))
+        act = pol.mean_np(obs.cpu().numpy()) if pol is not None else rng.uniform(-1, 1, (n, sim.nu))
         sim.step(_t(act), obs, rew, done, goal)
         sim.get_state(q, v)
         torch.cuda.synchronize()
-        _, r_ref, _, _, _ = o.step(st, act, nthreads=8)
+        _, r_ref, _, _, ost = o.step(st, act, nthreads=8)
+        ostatus |= int(np.bitwise_or.reduce(ost))
         qg, vg = q.cpu().numpy(), v.cpu().numpy()
         okq = (np.abs(qg - st["qpos"]) <= 2e-5 + 1e-5 * np.abs(st["qpos"])).all(axis=1)
         okv = (np.abs(vg - st["qvel"]) <= 5e-3 * (1 + np.abs(st["qvel"]))).all(axis=1)
         ok = okq & okv
         oks.append(ok)
-        rg = rew.cpu().numpy()
-        rok.append(np.abs(rg - r_ref)[ok] <= 1e-3 + 1e-3 * np.abs(r_ref[ok]))
+        rok.append(_rewards_close(rew.cpu().numpy(), r_ref, check=False))
     frac = np.concatenate(oks).mean()
-    print(f"teacher-forced {env_id} (disableflags {disableflags:#x}): {frac:.4f} of (env, step) cases "
-          f"within tolerance")
-    assert np.concatenate(rok).all(), env_id
+    rfrac = np.concatenate(rok).mean()
+    print(f"teacher-forced {env_id} (disableflags {disableflags:#x}{', DAPG policy' if policy else ''}): "
+          f"{frac:.4f} of {n * steps} (env, step) cases within the state tolerance, rewards {rfrac:.4f}")
+    assert not (ostatus & 24), "oracle overflowed MuJoCo's capacities"
+    _no_overflow(sim, n)
+    assert rfrac >= REWARD_MIN, (env_id, rfrac)
     return frac
 
 
@@ -318,7 +366,6 @@ def test_hammer_variations_one_step(variation):
     from mj_envs_amd.tasks import sample_params
     env_id, n = "hammer-v0", 64
     m, o = make_oracle(env_id, variation)
-    o.set_option(max_con=32, max_efc=128)
     rng = np.random.default_rng(21)
     P = sample_params(env_id, m, rng, n, variation)
     st, obs_ref = o.reset(P)
@@ -340,9 +387,8 @@ def test_hammer_variations_one_step(variation):
     okq = (np.abs(q - st["qpos"]) <= 2e-5 + 1e-5 * np.abs(st["qpos"])).all(axis=1)
     okv = (np.abs(v - st["qvel"]) <= 5e-3 * (1 + np.abs(st["qvel"]))).all(axis=1)
     ok = okq & okv
-    # >= 0.9: with the head moved ('pos') the hammer often rests on its cylindrical head, and the
-    # fp32 MPR (default build) can settle on a side face of such shallow face-on-face contacts;
-    # the -DAW_MPR_FP64 build (MPR in fp64 like MuJoCo's libccd) has no such case here (0 / 64)
-    assert ok.mean() >= 0.9, (variation, np.where(~ok)[0])
+    print(f"variation {variation}: {ok.mean():.4f} of {n} envs within tolerance")
+    assert ok.mean() >= VARIATION_MIN, (variation, np.where(~ok)[0])
+    _no_overflow(sim, n)
     np.testing.assert_allclose(obs.cpu().numpy()[ok], o_ref[ok], rtol=1e-3, atol=2e-3)
-    np.testing.assert_allclose(rew.cpu().numpy()[ok], r_ref[ok], rtol=1e-3, atol=1e-3)
+    _rewards_close(rew.cpu().numpy(), r_ref)

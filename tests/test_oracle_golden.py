@@ -66,3 +66,23 @@ def test_reset_draws_match_reference(tag, env_id, var):
     rng = np.random.default_rng(int(g["seed"]))
     p = sample_params(env_id, m, rng, g["params"].shape[0], var)
     np.testing.assert_allclose(p, g["params"], rtol=0, atol=1e-15)
+
+
+@pytest.mark.parametrize("env_id", ENVS)
+def test_env_state_semantics_match_reference(env_id):
+    """get_env_state / set_env_state (hammer_v0.py:134-153, door_v0.py:121-138,
+    pen_v0.py:134-152, relocate_v0.py:105-129): the dict the reference returns, and the model
+    fields its set_env_state writes on a fresh env (tests/golden/state_*.npz)."""
+    from mj_envs_amd.tasks import default_params, env_state_from, env_state_to_params, load_model
+    model = load_model(env_id)
+    g = golden(f"state_{env_id.split('-')[0]}.npz")
+    keys = sorted(k[4:] for k in g.files if k.startswith("get_"))
+    for i in range(g["qpos"].shape[0]):
+        st = env_state_from(env_id, model, g["qpos"][i], g["qvel"][i], g["params_before"][i],
+                            xpos=g["xpos"][i], site_xpos=g["site_xpos"][i])
+        assert sorted(st) == keys
+        for k in keys:
+            np.testing.assert_array_equal(st[k], g["get_" + k][i])
+        p = env_state_to_params(env_id, st, default_params(env_id, model))
+        np.testing.assert_array_equal(p, g["params_after"][i])
+        np.testing.assert_array_equal(g["qpos_after"][i], g["qpos"][i])

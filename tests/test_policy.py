@@ -81,10 +81,10 @@ def test_gpu_closed_loop_hammer():
         pol.act(obs, out=act, sample=True, seed=1, step=k)
         sim.step(act, obs, rew, done, goal, autoreset=True, seed=2)
     flags = sim.empty(n, dtype=torch.int32)
-    sim.status(flags)
+    sim.status(sticky=flags)
     eps = sim.empty(n, dtype=torch.int32)
     sim.episode_stats(episodes=eps)
     torch.cuda.synchronize()
     assert torch.isfinite(obs).all()
-    assert (flags.cpu().numpy() & 7 == 0).all()
+    assert (flags.cpu().numpy() == 0).all()        # no bad state, no capacity overflow
     assert (eps.cpu().numpy() == 1).all()          # every env finished exactly one episode

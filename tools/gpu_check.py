@@ -24,7 +24,7 @@ def check(env, n=4, steps=3, dsbl=0):
     sim = _native.Sim(blob, n)
     orc = Oracle(blob)
     sim.set_option(disableflags=dsbl)
-    orc.set_option(disableflags=dsbl, max_con=32, max_efc=128)
+    orc.set_option(disableflags=dsbl)
     params = sample_params(env, m, np.random.default_rng(0), n)
     pt = torch.tensor(params, dtype=torch.float32, device="cuda")
     obs = sim.empty(n, sim.obs_dim)

@@ -19,7 +19,6 @@ from oracle.pyoracle import Oracle  # noqa: E402
 def main(env_id="hammer-v0", n=32, steps=200, seed=0):
     m = attach_task(load_model(env_id), env_id)
     o = Oracle(m.to_blob())
-    o.set_option(max_con=32, max_efc=128)
     rng = np.random.default_rng(seed)
     P = sample_params(env_id, m, rng, n)
     st, _ = o.reset(P)
