@@ -165,6 +165,16 @@ int aw_render_depth(aw_handle* h, const float* cam, int width, int height, float
 int aw_policy_mlp(int n, int in_dim, int hidden, int out_dim, const float* params, const float* obs,
                   float* act, int sample, uint64_t seed, uint64_t step, uint64_t env_offset, void* stream);
 
+/* Test hook: the narrowphase collider of n primitive pairs given world poses (device arrays):
+ * types [n][2] (MuJoCo mjtGeom: plane 0, sphere 2, capsule 3, cylinder 5, box 6), pos [n][2][3],
+ * mat [n][2][9] (row-major rotations), size [n][2][3], margin [n] -> count [n] and out
+ * [n][AW_MAXPAIRCON][7] = (dist, pos[3], normal[3]) in emission order, the normal pointing from
+ * the lower-type geom to the other (MuJoCo's geom1 -> geom2).  The MPR collider runs at the
+ * handle's precision.  Used by the exact-geometry collider tests against the oracle. */
+#define AW_MAXPAIRCON 8
+int aw_collide_test(aw_handle* h, int n, const int32_t* types, const float* pos, const float* mat,
+                    const float* size, const float* margin, float* out, int32_t* count, void* stream);
+
 /* Diagnostic: per-stage shader-clock cycles of k_step summed over all waves since the last
  * reset (40 counters, see aw_common.h PR_*).  Only libraries built with -DAW_STAGE_PROF
  * collect them; the product build returns AW_EUNSUPPORTED. */

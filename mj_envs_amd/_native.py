@@ -77,6 +77,8 @@ def load():
     L.aw_task_eval.argtypes = [_vp, ctypes.c_int] + [_vp] * 10 + [_vp]
     L.aw_forward_dump.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp]
     L.aw_stage_profile.argtypes = [_vp, ctypes.c_int]
+    L.aw_collide_test.argtypes = [_vp, ctypes.c_int] + [_vp] * 7 + [_vp, _vp]
+    L.aw_collide_test.restype = ctypes.c_int
     # (diagnostic builds of older revisions, selected with AW_LIB, may lack the newer entry points;
     # calling one of those then raises AttributeError)
     if hasattr(L, "aw_render_depth"):
@@ -99,7 +101,7 @@ EXPORTS = ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "a
            "aw_random_actions", "aw_set_env_offset", "aw_get_state", "aw_set_state", "aw_status",
            "aw_clear_status", "aw_episode_stats", "aw_episode_totals", "aw_get_episode", "aw_set_episode",
            "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_render_depth", "aw_policy_mlp",
-           "aw_last_error")
+           "aw_collide_test", "aw_last_error")
 
 STAGES = ("pre", "kinematics", "collision", "com_crb", "rne_smooth_solve", "constraints", "newton",
           "noslip", "jt_touch", "euler", "task_obs", "reset", "checks")
@@ -235,6 +237,19 @@ class Sim:
         c = np.ascontiguousarray(cam, np.float32)
         assert c.size == 17, "render_depth: camera record has 17 floats"
         _check(load().aw_render_depth(self.h, c.ctypes.data, w, h, _ptr(out), _stream()))
+
+    def collide_test(self, types, pos, mat, size, margin):
+        """narrowphase of n primitive pairs (test hook): list of arrays [(dist, pos[3], normal[3]), ...]"""
+        import torch
+        n = len(types)
+        dev = self.torch_device
+        t = lambda a, dt=torch.float32: torch.tensor(np.asarray(a), dtype=dt, device=dev).contiguous()
+        out = torch.zeros(n, 8, 7, device=dev)
+        cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+        _check(load().aw_collide_test(self.h, n, _ptr(t(types, torch.int32)), _ptr(t(pos)), _ptr(t(mat)),
+                                      _ptr(t(size)), _ptr(t(margin)), _ptr(out), _ptr(cnt), _stream()))
+        o, c = out.cpu().numpy().astype(np.float64), cnt.cpu().numpy()
+        return [o[i, :c[i]] for i in range(n)]
 
     def forward_dump(self, env: int, ctrl=None) -> dict:
         import torch

@@ -538,6 +538,63 @@ __global__ void __launch_bounds__(64) k_task_eval(DModel m, int n, const float* 
   }
 }
 
+// Test hook (aw_collide_test): the narrowphase of one primitive pair per workgroup, given world
+// poses -- exact-geometry collider tests against the oracle's colliders.
+template <int MP>
+AW_DEV void collide_gv(const DModel& m, const GV& a, const GV& b, float margin, Emit& e) {
+  const int lo = a.type, hi = b.type;   // a.type <= b.type
+  if (lo == GEOM_PLANE) {
+    if (hi == GEOM_SPHERE) c_plane_sphere(a.pos, a.mat, b.pos, b.size[0], margin, e);
+    else if (hi == GEOM_CAPSULE) c_plane_capsule(a, b, margin, e);
+    else if (hi == GEOM_CYLINDER) c_plane_cylinder(a, b, margin, e);
+    else if (hi == GEOM_BOX) c_plane_box(a, b, margin, e);
+  } else if (lo == GEOM_CYLINDER || hi == GEOM_CYLINDER) {
+    if (MP) c_convex<double>(m, a, b, margin, e);
+    else c_convex<float>(m, a, b, margin, e);
+  } else if (hi == GEOM_BOX && lo == GEOM_BOX) {
+    c_box_box(a, b, margin, e);
+  } else if (hi == GEOM_BOX) {
+    if (lo == GEOM_SPHERE) c_sphere_box_pt(a.pos, a.size[0], b, margin, e);
+    else c_capsule_box(a, b, margin, e);
+  } else if (lo == GEOM_SPHERE && hi == GEOM_SPHERE) {
+    c_sphere_sphere(a.pos, a.size[0], b.pos, b.size[0], margin, e);
+  } else if (lo == GEOM_SPHERE) {
+    c_sphere_capsule(a, b, margin, e);
+  } else {
+    c_capsule_capsule(a, b, margin, e);
+  }
+}
+
+template <int MP>
+__global__ void __launch_bounds__(64) k_collide_test(DModel m, int n, const int* types, const float* pos,
+                                                     const float* mat, const float* size, const float* margin,
+                                                     float* out, int* count) {
+  __shared__ Env s;
+  const int i = blockIdx.x, lane = threadIdx.x;
+  if (i >= n) return;
+  if (lane == 0) { s.ncon = 0; s.status = 0u; }
+  wsync();
+  if (lane == 0) {
+    GV g[2];
+    for (int q = 0; q < 2; q++) {
+      g[q].type = types[2 * i + q];
+      for (int k = 0; k < 3; k++) { g[q].pos[k] = pos[6 * i + 3 * q + k]; g[q].size[k] = size[6 * i + 3 * q + k]; }
+      for (int k = 0; k < 9; k++) g[q].mat[k] = mat[18 * i + 9 * q + k];
+    }
+    const int f = g[0].type <= g[1].type ? 0 : 1;
+    Emit e{&s, 0, 0};
+    collide_gv<MP>(m, g[f], g[1 - f], margin[i], e);
+  }
+  wsync();
+  const int nc = s.ncon < MAXPAIRCON ? s.ncon : MAXPAIRCON;
+  if (lane == 0) count[i] = nc;
+  if (lane < nc) {
+    float* o = out + ((size_t)i * MAXPAIRCON + s.con_key[lane]) * 7;   // emission order
+    o[0] = s.con_dist[lane];
+    for (int k = 0; k < 3; k++) { o[1 + k] = s.con_pos[lane][k]; o[4 + k] = s.con_nrm[lane][k]; }
+  }
+}
+
 // depth frame of every env's current state: wave 0 runs the kinematics, then all four waves
 // cast the pixels (one workgroup per env; render geom poses staged in LDS)
 struct CamRec {
@@ -709,6 +766,11 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
   PUT(jnt_pos, tof(B.f("jnt_pos"))); PUT(jnt_axis, tof(B.f("jnt_axis")));
   PUT(jnt_range, tof(B.f("jnt_range"))); PUT(jnt_margin, tof(B.f("jnt_margin")));
   PUT(jnt_solref, tof(B.f("jnt_solref"))); PUT(jnt_solimp, tof(B.f("jnt_solimp")));
+  {
+    std::vector<double> r = B.f("jnt_range"), mg = B.f("jnt_margin"), off(2 * njnt);
+    for (int j = 0; j < njnt; j++) { off[2 * j] = r[2 * j] + mg[j]; off[2 * j + 1] = r[2 * j + 1] - mg[j]; }
+    PUT(jnt_limoff, tof(off));
+  }
 
   // actuators (joint transmission, one per dof)
   std::vector<int> trn = B.i("actuator_trnid");
@@ -766,6 +828,11 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
   PUT(ten_c0, c0); PUT(ten_c1, c1); PUT(ten_range, tof(B.f("tendon_range")));
   PUT(ten_margin, tof(B.f("tendon_margin"))); PUT(ten_solref, tof(B.f("tendon_solref")));
   PUT(ten_solimp, tof(B.f("tendon_solimp"))); PUT(ten_invweight0, tof(B.f("tendon_invweight0")));
+  {
+    std::vector<double> r = B.f("tendon_range"), mg = B.f("tendon_margin"), off(2 * ntendon);
+    for (int t = 0; t < ntendon; t++) { off[2 * t] = r[2 * t] + mg[t]; off[2 * t + 1] = r[2 * t + 1] - mg[t]; }
+    PUT(ten_limoff, tof(off));
+  }
 
   std::vector<double> gain = B.f("actuator_gainprm");
   std::vector<float> g0(nu);
@@ -1227,6 +1294,20 @@ int aw_policy_mlp(int n, int in_dim, int hidden, int out_dim, const float* param
     case 64: hipLaunchKernelGGL(k_mlp<64>, dim3(nb), dim3(bs), 0, st, n, in_dim, out_dim, params, obs, act, sample, seed, step, env_offset); break;
     default: return fail(AW_EUNSUPPORTED, "aw_policy_mlp: hidden width must be 32 or 64 (two hidden layers)");
   }
+  HIPCHK(hipGetLastError());
+  return AW_OK;
+}
+
+int aw_collide_test(aw_handle* h, int n, const int32_t* types, const float* pos, const float* mat, const float* size,
+                    const float* margin, float* out, int32_t* count, void* stream) {
+  if (!h || n <= 0 || !types || !pos || !mat || !size || !margin || !out || !count)
+    return fail(AW_EINVAL, "aw_collide_test: bad arguments");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  if (mpr_kernel_fp64(h))
+    hipLaunchKernelGGL(k_collide_test<1>, dim3(n), dim3(64), 0, st, h->m, n, types, pos, mat, size, margin, out, count);
+  else
+    hipLaunchKernelGGL(k_collide_test<0>, dim3(n), dim3(64), 0, st, h->m, n, types, pos, mat, size, margin, out, count);
   HIPCHK(hipGetLastError());
   return AW_OK;
 }

@@ -214,51 +214,118 @@ AW_DEV void c_sphere_box_pt(const float* p, float r, const GV& b, float margin, 
   emit(e, dist, pos, n);
 }
 
+// signed distance of the box-frame point c + t u to the box of half-sizes s (< 0 inside)
+AW_DEV float seg_box_f(const float* c, const float* u, const float* s, float t) {
+  float out = 0.f, mx = -1e30f;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const float q = fabsf(fmaf(t, u[k], c[k])) - s[k];
+    const float qp = fmaxf(q, 0.f);
+    out = fmaf(qp, qp, out);
+    mx = fmaxf(mx, q);
+  }
+  return sqrtf(out) + fminf(mx, 0.f);
+}
+
+// capsule (a) vs box (b): mjc_CapsuleBox's construction, the fp64 statement is
+// oracle/collide.cc capsule_box (same steps, same candidates, same tie rules):
+//  1. t* = exact minimiser of the convex piecewise signed distance along the segment: ends,
+//     slab / zero crossings, stationary points of the 2- and 3-coordinate outside pieces,
+//     crossings of two inside pieces; ties to the smallest t;
+//  2. two or three coordinates outside at t* -> edge / corner -> one contact; otherwise face k;
+//  3. face: the segment part over face k is [lo, hi]; t* moves to the nearer end when that end
+//     is as close (parallel capsule) and the other end is the second point; both sphere-box
+//     contacts within the margin (flat on a face: two contacts at the clipped ends).
 AW_DEV void c_capsule_box(const GV& a, const GV& b, float margin, Emit& e) {
-  float ax[3], p[3];
+  float ax[3];
   axis_of(ax, a.mat, 2);
   const float h = a.size[1], r = a.size[0];
-  // the capsule axis in the box frame: q(t) = c + t u, so each signed-distance evaluation of
-  // the golden-section search is 3 FMAs + the box distance (no per-point rotation)
+  const float* sz = b.size;
   float dif[3], c[3], u[3];
   sub3(dif, a.pos, b.pos);
   mulmtv3(c, b.mat, dif);
   mulmtv3(u, b.mat, ax);
-  auto sd = [&](float t) {
-    float out = 0.f, mx = -1e30f;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const float q = fabsf(fmaf(t, u[k], c[k])) - b.size[k];
-      const float qp = fmaxf(q, 0.f);
-      out = fmaf(qp, qp, out);
-      mx = fmaxf(mx, q);
-    }
-    return sqrtf(out) + fminf(mx, 0.f);
+  float best_t = -h, best_f = seg_box_f(c, u, sz, -h);
+  auto cand = [&](float t) {
+    t = fminf(fmaxf(t, -h), h);
+    const float f = seg_box_f(c, u, sz, t);
+    const bool take = f < best_f || (f == best_f && t < best_t);
+    best_f = take ? f : best_f;
+    best_t = take ? t : best_t;
   };
-  const float gr = 0.6180339887498949f;
-  float lo = -h, hi = h;
-  float x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo);
-  float f1 = sd(x1), f2 = sd(x2);
-  // branch-free (lanes hold different pairs): select the shrunk bracket, evaluate one point
-  for (int it = 0; it < 40; it++) {
-    const bool l = f1 < f2;
-    const float nhi = l ? x2 : hi, nlo = l ? lo : x1;
-    const float nx1 = l ? nhi - gr * (nhi - nlo) : x2;
-    const float nx2 = l ? x1 : nlo + gr * (nhi - nlo);
-    const float fe = sd(l ? nx1 : nx2);
-    const float of1 = f1, of2 = f2;
-    f1 = l ? fe : of2;
-    f2 = l ? of1 : fe;
-    hi = nhi; lo = nlo; x1 = nx1; x2 = nx2;
+  cand(h);
+#pragma unroll
+  for (int j = 0; j < 3; j++)
+    if (fabsf(u[j]) > 1e-12f) {
+      const float iu = 1.0f / u[j];
+      cand((sz[j] - c[j]) * iu);
+      cand((-sz[j] - c[j]) * iu);
+      cand(-c[j] * iu);
+    }
+#pragma unroll
+  for (int code = 0; code < 27; code++) {
+    const int cd0 = code % 3, cd1 = (code / 3) % 3, cd2 = code / 9;
+    if ((cd0 != 0) + (cd1 != 0) + (cd2 != 0) < 2) continue;
+    const int cd[3] = {cd0, cd1, cd2};
+    float nu = 0.f, de = 0.f;
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+      if (cd[j]) {
+        const float sg = cd[j] == 1 ? 1.f : -1.f;
+        nu += (sz[j] * sg - c[j]) * u[j];
+        de += u[j] * u[j];
+      }
+    if (de > 1e-24f) cand(nu / de);
   }
-  const float ts = 0.5f * (lo + hi);
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = i + 1; j < 3; j++)
+#pragma unroll
+      for (int sc = 0; sc < 4; sc++) {
+        const float si = (sc & 1) ? -1.f : 1.f, sj = (sc & 2) ? -1.f : 1.f;
+        const float den = si * u[i] - sj * u[j];
+        if (fabsf(den) > 1e-12f) cand((sz[i] - sz[j] - si * c[i] + sj * c[j]) / den);
+      }
+  float ts = best_t;
+  int nout = 0, kout = 0, kin = 0;
+  float pen = 1e30f;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const float q = fabsf(fmaf(ts, u[k], c[k]));
+    if (q > sz[k]) { nout++; kout = k; }
+    if (sz[k] - q < pen) { pen = sz[k] - q; kin = k; }
+  }
+  float t2 = ts;
+  bool second = false;
+  if (nout <= 1) {
+    const int fk = nout == 1 ? kout : kin;
+    float lo = -h, hi = h;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      if (j == fk) continue;
+      if (fabsf(u[j]) > 1e-12f) {
+        float t0 = (-sz[j] - c[j]) / u[j], t1 = (sz[j] - c[j]) / u[j];
+        const float mn = fminf(t0, t1), mx = fmaxf(t0, t1);
+        lo = fmaxf(lo, mn);
+        hi = fminf(hi, mx);
+      } else if (fabsf(c[j]) > sz[j]) {
+        hi = lo - 1.f;
+      }
+    }
+    if (hi > lo) {
+      const float tol = 1e-6f * (h + r);
+      const float near_end = (ts - lo <= hi - ts) ? lo : hi, far_end = near_end == lo ? hi : lo;
+      if (near_end != ts && seg_box_f(c, u, sz, near_end) <= best_f + tol) ts = near_end;
+      t2 = far_end;
+      second = fabsf(t2 - ts) > 1e-6f * h;
+    }
+  }
+  float p[3];
   for (int k = 0; k < 3; k++) p[k] = a.pos[k] + ax[k] * ts;
-  int before = e.cnt;
   c_sphere_box_pt(p, r, b, margin, e);
-  if (e.cnt == before) return;
-  float te = ts > 0 ? -h : h;
-  if (fabsf(te - ts) > 1e-6f * (h + 1e-12f)) {
-    for (int k = 0; k < 3; k++) p[k] = a.pos[k] + ax[k] * te;
+  if (second) {
+    for (int k = 0; k < 3; k++) p[k] = a.pos[k] + ax[k] * t2;
     c_sphere_box_pt(p, r, b, margin, e);
   }
 }
@@ -713,9 +780,17 @@ template <class T> AW_DEV int penetration(const Ctx<T>& c, T* depth, T* dir, T* 
 
 template <class T>
 AW_DEV void c_convex(const DModel& m, const GV& a, const GV& b, float margin, Emit& e) {
+  // The portal is built in a frame centred on the pair (MPR is translation invariant): support
+  // points are then O(geom size) instead of O(1 m) world coordinates, so every support
+  // evaluation's rounding is ~size * eps instead of ~|x| * eps.  In fp32 that is the difference
+  // between portal jitter of ~3e-8 m and ~1e-9 m on shallow face-on-face contacts whose portals
+  // are ~1e-4 m across.
+  float c[3];
   mpr::GVdT<T> ad, bd;
   for (int k = 0; k < 3; k++) {
-    ad.pos[k] = a.pos[k]; ad.size[k] = a.size[k]; bd.pos[k] = b.pos[k]; bd.size[k] = b.size[k];
+    c[k] = 0.5f * (a.pos[k] + b.pos[k]);
+    ad.pos[k] = (T)(a.pos[k] - c[k]); ad.size[k] = a.size[k];
+    bd.pos[k] = (T)(b.pos[k] - c[k]); bd.size[k] = b.size[k];
   }
   for (int k = 0; k < 9; k++) { ad.mat[k] = a.mat[k]; bd.mat[k] = b.mat[k]; }
   ad.type = a.type; bd.type = b.type;
@@ -725,7 +800,7 @@ AW_DEV void c_convex(const DModel& m, const GV& a, const GV& b, float margin, Em
   if (dir[0] == 0 && dir[1] == 0 && dir[2] == 0) return;
   const float dist = margin - (float)depth;
   if (dist > margin) return;
-  const float pf[3] = {(float)pos[0], (float)pos[1], (float)pos[2]};
+  const float pf[3] = {(float)pos[0] + c[0], (float)pos[1] + c[1], (float)pos[2] + c[2]};
   const float df[3] = {(float)dir[0], (float)dir[1], (float)dir[2]};
   emit(e, dist, pf, df);
 }

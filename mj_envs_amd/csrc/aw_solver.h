@@ -197,16 +197,19 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
     s.efc_i0[lane] = d; s.efc_i1[lane] = -1; s.efc_v0[lane] = 1.f; s.efc_v1[lane] = 0.f;
     s.rowbuf[lane] = 0.f; s.efc_floss[lane] = MD(dof_frictionloss, d); s.efc_force[lane] = MD(dof_invweight0, d);
   }
-  // joint limits: lower then upper per joint, joints in order
+  // joint limits: lower then upper per joint, joints in order.  MuJoCo activates a side when
+  // dist = side * (range - q) < margin; that is evaluated as (range -+ margin) -+ q < 0 with the
+  // offset formed in fp64 on the host (jnt_limoff), so a joint resting at q ~ 0 whose range edge
+  // equals its margin (hammer's nail: range edge 0.01 = margin) is decided by the sign of q as in
+  // fp64 -- fp32 range - q would round a 1e-12 displacement away.  dlo / dhi are dist - margin.
   const bool lim = !(m.disableflags & DSBL_LIMIT);
   int lo = 0, hi = 0;
-  float dlo = 0, dhi = 0, mg = 0;
+  float dlo = 0, dhi = 0;
   if (lim && lane < m.njnt && MD(jnt_limited, lane)) {
     float q = s.qpos[lane];
-    mg = MD(jnt_margin, lane);
-    dlo = q - MD(jnt_range, 2 * lane);
-    dhi = MD(jnt_range, 2 * lane + 1) - q;
-    lo = dlo < mg; hi = dhi < mg;
+    dlo = q - MD(jnt_limoff, 2 * lane);
+    dhi = MD(jnt_limoff, 2 * lane + 1) - q;
+    lo = dlo < 0.f; hi = dhi < 0.f;
   }
   int njl;
   int off = nfl + wave_excl_scan(lo + hi, lane, &njl);
@@ -217,7 +220,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
       if (r >= MAXEFC) { atomicOr(&s.status, (unsigned)ST_EFC_OVERFLOW); continue; }
       s.efc_type[r] = C_LIM_JNT; s.efc_id[r] = lane;
       s.efc_i0[r] = lane; s.efc_i1[r] = -1; s.efc_v0[r] = side ? -1.f : 1.f; s.efc_v1[r] = 0.f;
-      s.rowbuf[r] = (side ? dhi : dlo) - mg; s.efc_floss[r] = 0.f; s.efc_force[r] = MD(dof_invweight0, lane);
+      s.rowbuf[r] = side ? dhi : dlo; s.efc_floss[r] = 0.f; s.efc_force[r] = MD(dof_invweight0, lane);
     }
   }
   // tendon limits
@@ -225,10 +228,9 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
   if (lim && lane < m.ntendon && MD(ten_limited, lane)) {
     const int d1 = MD(ten_d1, lane);
     float len = MD(ten_c0, lane) * s.qpos[MD(ten_d0, lane)] + (d1 >= 0 ? MD(ten_c1, lane) * s.qpos[d1] : 0.f);
-    mg = MD(ten_margin, lane);
-    dlo = len - MD(ten_range, 2 * lane);
-    dhi = MD(ten_range, 2 * lane + 1) - len;
-    lo = dlo < mg; hi = dhi < mg;
+    dlo = len - MD(ten_limoff, 2 * lane);
+    dhi = MD(ten_limoff, 2 * lane + 1) - len;
+    lo = dlo < 0.f; hi = dhi < 0.f;
   }
   int ntl;
   off = nfl + njl + wave_excl_scan(lo + hi, lane, &ntl);
@@ -241,7 +243,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
       s.efc_type[r] = C_LIM_TEN; s.efc_id[r] = lane;
       s.efc_i0[r] = MD(ten_d0, lane); s.efc_i1[r] = MD(ten_d1, lane);
       s.efc_v0[r] = sg * MD(ten_c0, lane); s.efc_v1[r] = sg * MD(ten_c1, lane);
-      s.rowbuf[r] = (side ? dhi : dlo) - mg; s.efc_floss[r] = 0.f; s.efc_force[r] = MD(ten_invweight0, lane);
+      s.rowbuf[r] = side ? dhi : dlo; s.efc_floss[r] = 0.f; s.efc_force[r] = MD(ten_invweight0, lane);
     }
   }
   int nsparse = nfl + njl + ntl;

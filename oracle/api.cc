@@ -189,6 +189,8 @@ int or_get1(void* p, const char* name, double* out, int cap) {
     tmp = {(double)d->ncon, (double)d->nefc, (double)d->solver_iter, (double)d->noslip_iter, (double)d->status};
   } else if (s == "efc_type") {
     for (int i = 0; i < d->nefc; i++) tmp.push_back(d->efc_type[i]);
+  } else if (s == "efc_id") {
+    for (int i = 0; i < d->nefc; i++) tmp.push_back(d->efc_id[i]);
   } else if (s == "efc_state") {
     for (int i = 0; i < d->nefc; i++) tmp.push_back(d->efc_state[i]);
   } else if (s == "contact") {
@@ -216,6 +218,21 @@ int or_get1(void* p, const char* name, double* out, int cap) {
   if (out)
     for (size_t i = 0; i < tmp.size() && (int)i < cap; i++) out[i] = tmp[i];
   return (int)tmp.size();
+}
+
+/* Test hook: narrowphase of two primitives (types, world positions, row-major rotation
+ * matrices, sizes) with the handle's MPR options.  out: up to 16 contacts x (dist, pos[3],
+ * normal[3]) pointing from the first-listed (lower type) geom to the other; returns the count. */
+int or_collide(void* p, int t1, const double* p1, const double* m1, const double* s1, int t2, const double* p2,
+               const double* m2, const double* s2, double margin, double* out) {
+  Handle* h = (Handle*)p;
+  Contact buf[16];
+  int n = collide_raw(&h->m, t1, p1, m1, s1, t2, p2, m2, s2, margin, buf);
+  for (int i = 0; i < n; i++) {
+    out[7 * i] = buf[i].dist;
+    for (int k = 0; k < 3; k++) { out[7 * i + 1 + k] = buf[i].pos[k]; out[7 * i + 4 + k] = buf[i].frame[k]; }
+  }
+  return n;
 }
 
 /* exposed for the golden-vector test of the task layer: quat2euler (quatmath.py:136) */

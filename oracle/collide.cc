@@ -235,50 +235,122 @@ static int sphere_box_pt(const num* p, num r, const GeomView& b, num margin, Con
   return 1;
 }
 
-static num box_sdist(const num* p, const GeomView& b) {
-  num dif[3], loc[3];
-  sub3(dif, p, b.pos);
-  mul_matT_vec3(loc, b.mat, dif);
-  num q[3], out = 0, mx = -1e300;
+/* Signed distance of the box-frame point c + t u to the box of half-sizes s (< 0 inside). */
+static num seg_box_f(const num* c, const num* u, const num* s, num t) {
+  num out = 0, mx = -1e300;
   for (int k = 0; k < 3; k++) {
-    q[k] = std::fabs(loc[k]) - b.size[k];
-    num qp = q[k] > 0 ? q[k] : 0;
+    num q = std::fabs(c[k] + t * u[k]) - s[k];
+    num qp = q > 0 ? q : 0;
     out += qp * qp;
-    mx = q[k] > mx ? q[k] : mx;
+    mx = q > mx ? q : mx;
   }
   return std::sqrt(out) + (mx < 0 ? mx : 0);
 }
 
+/* Exact minimiser of the (convex, piecewise) signed distance along the segment t in [-h, h]:
+ * the minimum lies at an end, at a breakpoint where a coordinate crosses a slab boundary or
+ * zero, at the stationary point of an outside piece (2 or 3 coordinates outside, fixed signs),
+ * or where two inside pieces |q_i| - s_i = |q_j| - s_j cross.  Every candidate is evaluated;
+ * ties go to the smallest t.  (Round 1 ran a 40-step golden-section search.) */
+static num seg_box_argmin(const num* c, const num* u, const num* s, num h, num* fmin) {
+  num best_t = -h, best_f = seg_box_f(c, u, s, -h);
+  auto cand = [&](num t) {
+    if (!(t > -h)) t = -h;
+    if (t > h) t = h;
+    num f = seg_box_f(c, u, s, t);
+    if (f < best_f || (f == best_f && t < best_t)) { best_f = f; best_t = t; }
+  };
+  cand(h);
+  for (int j = 0; j < 3; j++)
+    if (std::fabs(u[j]) > 1e-12) {
+      cand((s[j] - c[j]) / u[j]);
+      cand((-s[j] - c[j]) / u[j]);
+      cand(-c[j] / u[j]);
+    }
+  /* outside pieces: coordinate j outside with sign sg_j (code 1: +, 2: -), 0: not outside */
+  for (int code = 0; code < 27; code++) {
+    int cd[3] = {code % 3, (code / 3) % 3, code / 9};
+    int nout = (cd[0] != 0) + (cd[1] != 0) + (cd[2] != 0);
+    if (nout < 2) continue;
+    num num_ = 0, den = 0;
+    for (int j = 0; j < 3; j++)
+      if (cd[j]) {
+        num sg = cd[j] == 1 ? 1.0 : -1.0;
+        num_ += (s[j] * sg - c[j]) * u[j];
+        den += u[j] * u[j];
+      }
+    if (den > 1e-24) cand(num_ / den);
+  }
+  /* inside crossings */
+  for (int i = 0; i < 3; i++)
+    for (int j = i + 1; j < 3; j++)
+      for (int sc = 0; sc < 4; sc++) {
+        num si = (sc & 1) ? -1.0 : 1.0, sj = (sc & 2) ? -1.0 : 1.0;
+        num den = si * u[i] - sj * u[j];
+        if (std::fabs(den) > 1e-12) cand((s[i] - s[j] - si * c[i] + sj * c[j]) / den);
+      }
+  *fmin = best_f;
+  return best_t;
+}
+
+/* capsule (geom1) vs box (geom2), restating mjc_CapsuleBox's construction: the capsule is the
+ * segment inflated by its radius, so contacts are sphere-box contacts at chosen segment points.
+ * 1. t* = the segment point closest to (deepest in) the box (seg_box_argmin, box frame).
+ * 2. Closest box feature at t*: two or three coordinates outside their slabs -> an edge or a
+ *    corner -> one contact.  Otherwise a face k (the outside coordinate, or the face of least
+ *    penetration when inside).
+ * 3. Face: the part of the segment over face k (clipped to the face's other two slabs) is
+ *    [lo, hi].  If t* is interior to it and an end is as close (parallel capsule), t* moves to
+ *    that end; the second point is the other end.  Both become sphere-box contacts within the
+ *    margin: a capsule flat on a face gets two contacts at the clipped ends with the exact
+ *    depth, a capsule across an edge one. */
 static int capsule_box(const GeomView& g1, const GeomView& g2, num margin, Contact* c) {
-  num ax[3];
+  num ax[3], dif[3], cl[3], u[3];
   axis_of(ax, g1.mat, 2);
-  num h = g1.size[1], r = g1.size[0];
-  /* golden-section search for the minimum signed distance along the segment */
-  const num gr = 0.6180339887498949;
-  num a = -h, b = h, p[3];
-  num x1 = b - gr * (b - a), x2 = a + gr * (b - a);
-  for (int k = 0; k < 3; k++) p[k] = g1.pos[k] + ax[k] * x1;
-  num f1 = box_sdist(p, g2);
-  for (int k = 0; k < 3; k++) p[k] = g1.pos[k] + ax[k] * x2;
-  num f2 = box_sdist(p, g2);
-  for (int it = 0; it < 40; it++) {
-    if (f1 < f2) { b = x2; x2 = x1; f2 = f1; x1 = b - gr * (b - a);
-      for (int k = 0; k < 3; k++) p[k] = g1.pos[k] + ax[k] * x1;
-      f1 = box_sdist(p, g2);
-    } else { a = x1; x1 = x2; f1 = f2; x2 = a + gr * (b - a);
-      for (int k = 0; k < 3; k++) p[k] = g1.pos[k] + ax[k] * x2;
-      f2 = box_sdist(p, g2);
+  const num h = g1.size[1], r = g1.size[0];
+  const num* sz = g2.size;
+  sub3(dif, g1.pos, g2.pos);
+  mul_matT_vec3(cl, g2.mat, dif);
+  mul_matT_vec3(u, g2.mat, ax);
+  num fmin;
+  num ts = seg_box_argmin(cl, u, sz, h, &fmin);
+  int nout = 0, kout = 0, kin = 0;
+  num pen = 1e300;
+  for (int k = 0; k < 3; k++) {
+    num q = std::fabs(cl[k] + ts * u[k]);
+    if (q > sz[k]) { nout++; kout = k; }
+    if (sz[k] - q < pen) { pen = sz[k] - q; kin = k; }
+  }
+  num t2 = ts;
+  bool second = false;
+  if (nout <= 1) {
+    const int fk = nout == 1 ? kout : kin;
+    num lo = -h, hi = h;
+    for (int j = 0; j < 3; j++) {
+      if (j == fk) continue;
+      if (std::fabs(u[j]) > 1e-12) {
+        num a = (-sz[j] - cl[j]) / u[j], b = (sz[j] - cl[j]) / u[j];
+        if (a > b) std::swap(a, b);
+        lo = std::max(lo, a);
+        hi = std::min(hi, b);
+      } else if (std::fabs(cl[j]) > sz[j]) {
+        hi = lo - 1;   /* never over the face */
+      }
+    }
+    if (hi > lo) {
+      const num tol = 1e-6 * (h + r);
+      num near_end = (ts - lo <= hi - ts) ? lo : hi, far_end = near_end == lo ? hi : lo;
+      if (near_end != ts && seg_box_f(cl, u, sz, near_end) <= fmin + tol) ts = near_end;
+      t2 = far_end;
+      second = std::fabs(t2 - ts) > 1e-6 * h;
     }
   }
-  num ts = 0.5 * (a + b);
+  num p[3];
   for (int k = 0; k < 3; k++) p[k] = g1.pos[k] + ax[k] * ts;
   int n = sphere_box_pt(p, r, g2, margin, c);
-  if (n == 0) return 0;
-  /* second contact: the endpoint farther from the minimum */
-  num te = ts > 0 ? -h : h;
-  if (std::fabs(te - ts) > 1e-6 * (h + 1e-12)) {
-    for (int k = 0; k < 3; k++) p[k] = g1.pos[k] + ax[k] * te;
-    n += sphere_box_pt(p, r, g2, margin, c + 1);
+  if (second) {
+    for (int k = 0; k < 3; k++) p[k] = g1.pos[k] + ax[k] * t2;
+    n += sphere_box_pt(p, r, g2, margin, c + n);
   }
   return n;
 }
@@ -706,6 +778,8 @@ static int convex(const Model* m, const GeomView& g1, const GeomView& g2, num ma
 }
 
 /* ------------------------------------------------------------------------------------- */
+static int collide_views(const Model* m, GeomView a, GeomView b, num margin, Contact* out);
+
 int collide_geoms(const Model* m, const Data* d, int g1, int g2, num margin, Contact* out, int maxout) {
   (void)maxout;
   GeomView a{&d->geom_xpos[3 * g1], &d->geom_xmat[9 * g1], &d->geom_size[3 * g1], m->geom_type[g1]};
@@ -718,6 +792,18 @@ int collide_geoms(const Model* m, const Data* d, int g1, int g2, num margin, Con
     int gb = ga == g1 ? g2 : g1;
     if (norm3(dif) > m->geom_rbound[ga] + m->geom_rbound[gb] + margin) return 0;
   }
+  return collide_views(m, a, b, margin, out);
+}
+
+/* narrowphase of two primitives given by pose / size (test hook: exact-geometry collider tests) */
+int collide_raw(const Model* m, int t1, const num* p1, const num* m1, const num* s1, int t2, const num* p2,
+                const num* m2, const num* s2, num margin, Contact* out) {
+  GeomView a{p1, m1, s1, t1}, b{p2, m2, s2, t2};
+  if (a.type > b.type) { GeomView t = a; a = b; b = t; }
+  return collide_views(m, a, b, margin, out);
+}
+
+static int collide_views(const Model* m, GeomView a, GeomView b, num margin, Contact* out) {
   switch (a.type) {
     case GEOM_PLANE:
       switch (b.type) {

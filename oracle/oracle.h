@@ -160,6 +160,8 @@ void mul_M(const Model* m, const Data* d, const num* x, num* y);
 /* collide.cc */
 void collision(const Model* m, Data* d);
 int collide_geoms(const Model* m, const Data* d, int g1, int g2, num margin, Contact* out, int maxout);
+int collide_raw(const Model* m, int t1, const num* p1, const num* m1, const num* s1, int t2, const num* p2,
+                const num* m2, const num* s2, num margin, Contact* out);
 num ray_geom(const num* pos, const num* mat, const num* size, const num* pnt, const num* vec, int type);
 
 /* solver.cc */

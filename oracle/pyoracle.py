@@ -47,6 +47,8 @@ def lib():
         L.or_get1.argtypes = [ctypes.c_void_p, ctypes.c_char_p, _dp, ctypes.c_int]
         L.or_quat2euler.argtypes = [_dp, _dp]
         L.or_task_eval.argtypes = [ctypes.c_void_p, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _dp]
+        L.or_collide.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp, _dp, ctypes.c_int, _dp, _dp, _dp,
+                                 ctypes.c_double, _dp]
         _lib = L
     return _lib
 
@@ -128,6 +130,14 @@ class Oracle:
         out = np.zeros(max(n, 1))
         lib().or_get1(self.h, name.encode(), _p(out), n)
         return out[:n]
+
+    def collide(self, t1, pos1, mat1, size1, t2, pos2, mat2, size2, margin):
+        """narrowphase of two primitives (test hook): [(dist, pos[3], normal[3]), ...]"""
+        c = lambda a: np.ascontiguousarray(a, np.float64).ravel()
+        out = np.zeros(16 * 7)
+        n = lib().or_collide(self.h, int(t1), _p(c(pos1)), _p(c(mat1)), _p(c(size1)), int(t2), _p(c(pos2)),
+                             _p(c(mat2)), _p(c(size2)), float(margin), _p(out))
+        return out[:7 * n].reshape(n, 7)
 
     def task_eval(self, qpos, qvel, xpos, xquat, site_xpos, sensordata):
         c = lambda a: np.ascontiguousarray(a, np.float64).ravel()

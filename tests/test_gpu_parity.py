@@ -197,7 +197,13 @@ def test_random_actions_and_reset_sampling():
     sim.get_state(params=p)
     torch.cuda.synchronize()
     p = p.cpu().numpy()
-    for k, (lo, hi) in enumerate(reset_ranges("relocate-v0")):
+    from mj_envs_amd.tasks import param_draws
+    rr = reset_ranges("relocate-v0")
+    for k, c in enumerate(param_draws("relocate-v0")):
+        if c < 0:                         # not drawn at reset: keeps the model value
+            assert p[:, k].std() == 0
+            continue
+        lo, hi = rr[c]
         assert p[:, k].min() >= lo and p[:, k].max() <= hi
         assert p[:, k].std() > 0.2 * (hi - lo)
 
