@@ -77,7 +77,7 @@ def load():
     L.aw_task_eval.argtypes = [_vp, ctypes.c_int] + [_vp] * 10 + [_vp]
     L.aw_forward_dump.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp]
     L.aw_stage_profile.argtypes = [_vp, ctypes.c_int]
-    L.aw_collide_test.argtypes = [_vp, ctypes.c_int] + [_vp] * 7 + [_vp, _vp]
+    L.aw_collide_test.argtypes = [_vp, ctypes.c_int] + [_vp] * 8
     L.aw_collide_test.restype = ctypes.c_int
     # (diagnostic builds of older revisions, selected with AW_LIB, may lack the newer entry points;
     # calling one of those then raises AttributeError)

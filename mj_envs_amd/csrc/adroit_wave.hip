@@ -766,11 +766,7 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
   PUT(jnt_pos, tof(B.f("jnt_pos"))); PUT(jnt_axis, tof(B.f("jnt_axis")));
   PUT(jnt_range, tof(B.f("jnt_range"))); PUT(jnt_margin, tof(B.f("jnt_margin")));
   PUT(jnt_solref, tof(B.f("jnt_solref"))); PUT(jnt_solimp, tof(B.f("jnt_solimp")));
-  {
-    std::vector<double> r = B.f("jnt_range"), mg = B.f("jnt_margin"), off(2 * njnt);
-    for (int j = 0; j < njnt; j++) { off[2 * j] = r[2 * j] + mg[j]; off[2 * j + 1] = r[2 * j + 1] - mg[j]; }
-    PUT(jnt_limoff, tof(off));
-  }
+  PUT(jnt_range64, B.f("jnt_range")); PUT(jnt_margin64, B.f("jnt_margin"));
 
   // actuators (joint transmission, one per dof)
   std::vector<int> trn = B.i("actuator_trnid");
@@ -828,10 +824,11 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
   PUT(ten_c0, c0); PUT(ten_c1, c1); PUT(ten_range, tof(B.f("tendon_range")));
   PUT(ten_margin, tof(B.f("tendon_margin"))); PUT(ten_solref, tof(B.f("tendon_solref")));
   PUT(ten_solimp, tof(B.f("tendon_solimp"))); PUT(ten_invweight0, tof(B.f("tendon_invweight0")));
+  PUT(ten_range64, B.f("tendon_range")); PUT(ten_margin64, B.f("tendon_margin"));
   {
-    std::vector<double> r = B.f("tendon_range"), mg = B.f("tendon_margin"), off(2 * ntendon);
-    for (int t = 0; t < ntendon; t++) { off[2 * t] = r[2 * t] + mg[t]; off[2 * t + 1] = r[2 * t + 1] - mg[t]; }
-    PUT(ten_limoff, tof(off));
+    std::vector<double> a0(ntendon), a1(ntendon);
+    for (int t = 0; t < ntendon; t++) { a0[t] = wc[tadr[t]]; a1[t] = tnum[t] > 1 ? wc[tadr[t] + 1] : 0.0; }
+    PUT(ten_c0_64, a0); PUT(ten_c1_64, a1);
   }
 
   std::vector<double> gain = B.f("actuator_gainprm");

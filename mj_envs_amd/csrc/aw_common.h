@@ -113,8 +113,9 @@ constexpr int MAXRG = 64;     // rendered (primitive) geoms
   X(int, jnt_type, MAXV) X(int, jnt_bodyid, MAXV) X(int, jnt_limited, MAXV)                     \
   X(float, jnt_pos, MAXV * 3) X(float, jnt_axis, MAXV * 3) X(float, jnt_range, MAXV * 2)        \
   X(float, jnt_margin, MAXV) X(float, jnt_solref, MAXV * 2) X(float, jnt_solimp, MAXV * 5)      \
-  /* limit activation offsets, host fp64: (range_lo + margin, range_hi - margin) */              \
-  X(float, jnt_limoff, MAXV * 2) X(float, ten_limoff, MAXT * 2)                                 \
+  /* limit activation in fp64 (the reference's arithmetic): range, margin, tendon coefficients */ \
+  X(double, jnt_range64, MAXV * 2) X(double, jnt_margin64, MAXV) X(double, ten_range64, MAXT * 2) \
+  X(double, ten_margin64, MAXT) X(double, ten_c0_64, MAXT) X(double, ten_c1_64, MAXT)              \
   X(int, dof_bodyid, MAXV) X(int, dof_act, MAXV) /* actuator driving the dof or -1 */          \
   X(int, fl_dof, MAXV) X(int, fl_row, MAXV) /* frictionloss row r -> dof, dof -> row / -1 */   \
   X(unsigned long long, dof_ancmask, MAXV) /* strict ancestor dofs */                          \

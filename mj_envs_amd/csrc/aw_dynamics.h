@@ -87,10 +87,14 @@ AW_DEV void stage_kinematics(const DModel& m, Env& s, int lane) {
           for (int c = 0; c < 3; c++) xp[c] += xaxis[c] * q;
         } else {
           float sn, cs, ql[4], v[3];
-          // hardware v_sin / v_cos (|q / 2| <= pi here): the library sinf / cosf pair was ~80 VALU
-          // per hinge on the level sweep's critical path
-          sn = __sinf(0.5f * q);
-          cs = __cosf(0.5f * q);
+          // hardware v_sin / v_cos (the library sinf / cosf pair was ~80 VALU per hinge on the
+          // level sweep's critical path).  Their absolute error grows with |x|, and the object
+          // hinges (OBJRx/y/z) are unlimited, so the half angle is first reduced to [-pi, pi]:
+          // q/2 - 2 pi round(q / (4 pi)), exact enough for any reachable angle.
+          const float hq = 0.5f * q;
+          const float hr = fmaf(-6.28318530717958648f, rintf(hq * 0.159154943091895336f), hq);
+          sn = __sinf(hr);
+          cs = __cosf(hr);
           ql[0] = cs; ql[1] = axis[0] * sn; ql[2] = axis[1] * sn; ql[3] = axis[2] * sn;
           mulq(xq, xq, ql);
           rotvq(v, jp, xq);

@@ -198,18 +198,20 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
     s.rowbuf[lane] = 0.f; s.efc_floss[lane] = MD(dof_frictionloss, d); s.efc_force[lane] = MD(dof_invweight0, d);
   }
   // joint limits: lower then upper per joint, joints in order.  MuJoCo activates a side when
-  // dist = side * (range - q) < margin; that is evaluated as (range -+ margin) -+ q < 0 with the
-  // offset formed in fp64 on the host (jnt_limoff), so a joint resting at q ~ 0 whose range edge
-  // equals its margin (hammer's nail: range edge 0.01 = margin) is decided by the sign of q as in
-  // fp64 -- fp32 range - q would round a 1e-12 displacement away.  dlo / dhi are dist - margin.
+  // dist = side * (range - q) < margin, in fp64.  That test is evaluated here in fp64 too, on the
+  // fp32 state with the model's fp64 range / margin (jnt_range64): a joint resting on a range
+  // edge equal to its margin (hammer's nail: range edge 0.01 = margin, q ~ 1e-22) is then decided
+  // exactly as the reference decides it -- in fp32, range - q rounds the other way.  dlo / dhi
+  // are dist - margin.
   const bool lim = !(m.disableflags & DSBL_LIMIT);
   int lo = 0, hi = 0;
   float dlo = 0, dhi = 0;
   if (lim && lane < m.njnt && MD(jnt_limited, lane)) {
-    float q = s.qpos[lane];
-    dlo = q - MD(jnt_limoff, 2 * lane);
-    dhi = MD(jnt_limoff, 2 * lane + 1) - q;
-    lo = dlo < 0.f; hi = dhi < 0.f;
+    const double q = (double)s.qpos[lane], mgd = MD(jnt_margin64, lane);
+    const double d0 = __dsub_rn(q, MD(jnt_range64, 2 * lane));
+    const double d1 = __dsub_rn(MD(jnt_range64, 2 * lane + 1), q);
+    lo = d0 < mgd; hi = d1 < mgd;
+    dlo = (float)(d0 - mgd); dhi = (float)(d1 - mgd);
   }
   int njl;
   int off = nfl + wave_excl_scan(lo + hi, lane, &njl);
@@ -227,10 +229,14 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
   lo = hi = 0;
   if (lim && lane < m.ntendon && MD(ten_limited, lane)) {
     const int d1 = MD(ten_d1, lane);
-    float len = MD(ten_c0, lane) * s.qpos[MD(ten_d0, lane)] + (d1 >= 0 ? MD(ten_c1, lane) * s.qpos[d1] : 0.f);
-    dlo = len - MD(ten_limoff, 2 * lane);
-    dhi = MD(ten_limoff, 2 * lane + 1) - len;
-    lo = dlo < 0.f; hi = dhi < 0.f;
+    // fixed tendon length in fp64 with the reference's operation order (no contraction)
+    const double len = __dadd_rn(__dmul_rn(MD(ten_c0_64, lane), (double)s.qpos[MD(ten_d0, lane)]),
+                                 d1 >= 0 ? __dmul_rn(MD(ten_c1_64, lane), (double)s.qpos[d1]) : 0.0);
+    const double mgd = MD(ten_margin64, lane);
+    const double e0 = __dsub_rn(len, MD(ten_range64, 2 * lane));
+    const double e1 = __dsub_rn(MD(ten_range64, 2 * lane + 1), len);
+    lo = e0 < mgd; hi = e1 < mgd;
+    dlo = (float)(e0 - mgd); dhi = (float)(e1 - mgd);
   }
   int ntl;
   off = nfl + njl + wave_excl_scan(lo + hi, lane, &ntl);

@@ -20,12 +20,15 @@ counterpart (the reference returns RGB), so this path is parity-unpinned against
 reference; it is checked against an independent numpy ray caster on the fp64 oracle's
 kinematics (``oracle/depth.py``, ``tests/test_render.py``).
 
-Reference quirks kept: hammer sets up its observer while ``obj_bid`` is still the placeholder
-``-1`` (``hammer_v0.py:15,35-38``), so the elevation uses the LAST body; door / pen / relocate
-construct their observer with placeholder body 0 (``door_v0.py:16,41``, ``pen_v0.py:13,44``,
-``relocate_v0.py:14,32``) and never call its setup -- the build applies the same camera
-construction with body 0 for them.  Meshes (the hand's visual geoms) are not available offline;
-the primitive collision proxies are rendered in their place.
+Reference quirks kept: hammer sets up its observer once, in ``__init__``, while ``obj_bid`` is
+still the placeholder ``-1`` (``hammer_v0.py:15,35-38``), so the elevation uses the LAST body.
+door and relocate construct their observer with placeholder body 0 (``door_v0.py:16,41``,
+``relocate_v0.py:14,32``) and call its setup on EVERY reset (``door_v0.py:114``,
+``relocate_v0.py:98``): body 0 is the world, so the camera is the same each time.  pen overrides
+``mj_viewer_headless_setup`` (its second definition, ``pen_v0.py:163-177``, wins) and calls it on
+every reset (``:127``) with ``target_obj_bid``, the 'target' body, whose position reset never
+moves (only its orientation is drawn).  Meshes (the hand's visual geoms) are not available
+offline; the primitive collision proxies are rendered in their place.
 """
 from __future__ import annotations
 
@@ -39,7 +42,7 @@ CAM_FLOATS = 17
 ZFAR = 10.0
 FULL_W, FULL_H, CROP = 640, 480, 128
 FOVY_DEG = 45.0                    # MuJoCo default visual/global/fovy
-OBS_BID = {"hammer-v0": -1, "door-v0": 0, "pen-v0": 0, "relocate-v0": 0}
+OBS_BID = {"hammer-v0": -1, "door-v0": 0, "pen-v0": "target", "relocate-v0": 0}   # body id or name
 
 
 def _geom_world0(model):
@@ -61,7 +64,10 @@ def free_camera(model, env_id: str, width: int = 64, height: int = 64, zfar: flo
     cam_b = int(model.cam_bodyid[-1]) if len(model.cam_bodyid) else 0
     xq = _kinematics0(model)[1][cam_b]
     cam_world = xpos[cam_b] + quat2mat(xq) @ cam
-    v = xpos[OBS_BID.get(env_id, 0)] - cam_world
+    bid = OBS_BID.get(env_id, 0)
+    if isinstance(bid, str):
+        bid = model.name2id("body", bid)
+    v = xpos[bid] - cam_world
     ratio = float(np.clip(v[0] / v[2], -1.0, 1.0)) if v[2] != 0 else 0.0
     elevation = -45.0 + math.degrees(math.acos(ratio)) / 2.0
     azimuth, distance = 90.0, 4.5

@@ -1,6 +1,6 @@
 """Attribute teacher-forced parity misses to a substep and a contact (GPU box diagnostic).
 
-    python tools/diag_tf.py <env_id> [dapg|random] [steps] [n_envs] [max_cases] [disableflags]
+    python tools/diag_tf.py <env_id> [dapg|random] [steps] [n_envs] [max_cases] [disableflags] [variation]
 
 Runs the teacher-forced rollout of tests/test_gpu_parity.py (GPU env-steps, each re-run by the
 fp64 oracle from the GPU's own pre-step state).  For each (env, step) outside the one-step
@@ -37,8 +37,8 @@ def gname(m, g):
     return f"{m.names['geom'][g] or g}:{TYPES.get(int(m.geom_type[g]), m.geom_type[g])}"
 
 
-def main(env_id="hammer-v0", pol_kind="dapg", steps=80, n=64, max_cases=12, dsbl=0):
-    m = attach_task(load_model(env_id), env_id)
+def main(env_id="hammer-v0", pol_kind="dapg", steps=80, n=64, max_cases=12, dsbl=0, variation=None):
+    m = attach_task(load_model(env_id), env_id, variation)
     blob = m.to_blob()
     o = Oracle(blob)
     pg = pair_geoms(m)
@@ -48,7 +48,7 @@ def main(env_id="hammer-v0", pol_kind="dapg", steps=80, n=64, max_cases=12, dsbl
         sim.set_option(disableflags=dsbl)
         one.set_option(disableflags=dsbl)
         o.set_option(disableflags=dsbl & 0xFFFF)
-    P = sample_params(env_id, m, np.random.default_rng(11), n)
+    P = sample_params(env_id, m, np.random.default_rng(11), n, variation)
     obs = sim.empty(n, sim.obs_dim)
     t = lambda a: torch.tensor(np.asarray(a), dtype=torch.float32, device="cuda")
     sim.reset(obs, params=t(P))
@@ -116,11 +116,13 @@ def main(env_id="hammer-v0", pol_kind="dapg", steps=80, n=64, max_cases=12, dsbl
         report.append(rec)
         print(json.dumps(rec), flush=True)
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(REPO, "gpurun_out", f"diag_{env_id.split('-')[0]}_{pol_kind}.json"), "w") as f:
+    tag = f"{env_id.split('-')[0]}_{pol_kind}" + (f"_{variation}" if variation else "") + (f"_{dsbl:#x}" if dsbl else "")
+    with open(os.path.join(REPO, "gpurun_out", f"diag_{tag}.json"), "w") as f:
         json.dump(dict(env_id=env_id, policy=pol_kind, n=n, steps=steps, misses=len(cases), cases=report), f, indent=1)
 
 
 if __name__ == "__main__":
     a = sys.argv[1:]
     main(a[0] if a else "hammer-v0", a[1] if len(a) > 1 else "dapg", int(a[2]) if len(a) > 2 else 80,
-         int(a[3]) if len(a) > 3 else 64, int(a[4]) if len(a) > 4 else 12, int(a[5], 0) if len(a) > 5 else 0)
+         int(a[3]) if len(a) > 3 else 64, int(a[4]) if len(a) > 4 else 12, int(a[5], 0) if len(a) > 5 else 0,
+         a[6] if len(a) > 6 else None)
