@@ -246,8 +246,8 @@ class Sim:
         t = lambda a, dt=torch.float32: torch.tensor(np.asarray(a), dtype=dt, device=dev).contiguous()
         out = torch.zeros(n, 8, 7, device=dev)
         cnt = torch.zeros(n, dtype=torch.int32, device=dev)
-        _check(load().aw_collide_test(self.h, n, _ptr(t(types, torch.int32)), _ptr(t(pos)), _ptr(t(mat)),
-                                      _ptr(t(size)), _ptr(t(margin)), _ptr(out), _ptr(cnt), _stream()))
+        args = [t(types, torch.int32), t(pos), t(mat), t(size), t(margin)]   # alive until the kernel ran
+        _check(load().aw_collide_test(self.h, n, *[_ptr(a) for a in args], _ptr(out), _ptr(cnt), _stream()))
         o, c = out.cpu().numpy().astype(np.float64), cnt.cpu().numpy()
         return [o[i, :c[i]] for i in range(n)]
 

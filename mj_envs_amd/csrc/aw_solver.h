@@ -462,7 +462,37 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
   float grad = gradient();
   AW_PROF(s, PR_NT_INIT);
   int iter = 0;
+  // The Hessian factor persists across iterations in LDS (s.L, packed rows; the backward solve
+  // reads it there anyway).  An iteration in which no row changed its quadratic state has the
+  // same Hessian as the previous one: its factor is reloaded instead of rebuilt (4 % of k_step on
+  // the A/B; rank-1 up / downdates for a few changed rows measured slower than refactoring).
+  float invd = 1.f;
+  bool inH[NRL];
+#pragma unroll
+  for (int h = 0; h < NRL; h++) inH[h] = false;
+  const int li = lane < NV ? lane : NV - 1;
   for (; iter < m.iterations; iter++) {
+    float H[NV];
+    bool full = iter == 0;
+    if (!full) {
+      bool chg = false;
+#pragma unroll
+      for (int h = 0; h < NRL; h++) chg |= rr[h].valid && ((rr[h].st == S_QUAD) != inH[h]);
+      full = __ballot(chg) != 0ull;
+    }
+    if (!full) {
+      // this lane's factor row from LDS (16-byte reads; entries above the diagonal are padding)
+      const float* Lr = &s.L[tri(li)];
+#pragma unroll
+      for (int q = 0; q < (NV + 3) / 4; q++) {
+        const float4 v = q * 4 <= li ? *reinterpret_cast<const float4*>(Lr + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+          if (4 * q + t < NV) H[4 * q + t] = vv[t];
+      }
+    }
+    if (full) {
     // Hessian H = M + J' D_quad J.  Sparse rows: diagonal terms gathered through an LDS vector,
     // the off-diagonal term of a two-dof (tendon) row added in registers by the two lanes it
     // couples; dense rows: rank-1 updates with the row broadcast from LDS.
@@ -486,8 +516,6 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
       offd[h] = __ballot(od);
     }
     wsync();
-    float H[NV];
-    const int li = lane < NV ? lane : NV - 1;
     {
       const float dg = s.hdiag[li];
 #pragma unroll
@@ -528,10 +556,12 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
     }
     wsync();
     AW_PROF(s, PR_NT_HESS);
-    float invd = 1.f;
     chol_factor<NV>(H, lane, invd, s);
     chol_store<NV>(H, lane, s);
     wsync();
+    }
+#pragma unroll
+    for (int h = 0; h < NRL; h++) inH[h] = rr[h].valid && rr[h].st == S_QUAD;
     AW_PROF(s, PR_NT_CHOL);
     float p = -chol_solve<NV>(H, invd, grad, lane, s);
     AW_PROF(s, PR_NT_SOLVE);
@@ -658,6 +688,9 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
   // per-dof-lane constants of the frictionloss row of that dof (lane d owns row fl_row[d])
   float fl_aref = 0.f, fl_lim = 0.f, fl_A = 1.f, fl_invA = 0.f;
   bool fl_ok;
+#ifndef AW_NOSLIP_SLOWCHAIN
+  float fl_c = 0.f;   // ffl + aref / A: the proposal is med3(fl_c - qacc / A, -lim, lim)
+#endif
   {
     float dg = 0.f;   // inv(M)[lane][lane]
 #pragma unroll
@@ -672,6 +705,11 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
       fl_A = dg;
       fl_invA = 1.0f / dg;
     }
+#ifndef AW_NOSLIP_SLOWCHAIN
+    // lanes without an active row propose their own force back (dl = 0 exactly): invA 0, no clamp
+    if (!fl_ok) { fl_invA = 0.f; fl_lim = 3.0e38f; }
+    fl_c = fmaf(fl_aref, fl_invA, ffl);
+#endif
   }
   // dense-row forces: row lane in fd, row 64 + lane in fd_hi (ndense <= MAXDENSE = 128)
   float fd_hi = 0.f;
@@ -744,6 +782,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
     // of its own row against the current qacc; step d keeps lane d's.  Lanes without an
     // active row propose exactly zero (branch-free).
     float imp_l = 0.f;
+#ifdef AW_NOSLIP_SLOWCHAIN
 #pragma unroll
     for (int d = 0; d < NV; d++) {
       const float r = qacc - fl_aref;
@@ -756,6 +795,21 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
       }
       qacc = fmaf(Mi[d], delta, qacc);
     }
+#else
+    // the serial chain per row: fma -> med3 -> sub -> readlane -> fma (was 8 dependent ops)
+#pragma unroll
+    for (int d = 0; d < NV; d++) {
+      const float x = __builtin_amdgcn_fmed3f(fmaf(-qacc, fl_invA, fl_c), -fl_lim, fl_lim);
+      const float dl = x - ffl;
+      const float delta = rlane(dl, d);
+      if (lane == d) {
+        imp_l += (qacc - fl_aref) * dl + 0.5f * fl_A * dl * dl;
+        ffl = x;
+        fl_c = fmaf(fl_aref, fl_invA, x);
+      }
+      qacc = fmaf(Mi[d], delta, qacc);
+    }
+#endif
     impr -= wave_sum(imp_l);
     // opposing pyramid-edge pairs, in row order (branch-free: a zero update is an exact no-op)
     auto pair_step = [&](int p, float j1, float j2, float x1, float x2) {

@@ -85,15 +85,11 @@ VARIATION_MIN = 0.9     # 'pos' (measured 0.94): the hammer rests on its moved c
                         # miss must be a discrete event (_discrete_event)
 REWARD_MIN = 0.995
 
-# Grasp regime (DAPG policies; hammer: fingers closed on the handle, head striking the nail).
-# Resting contacts sit AT their margin by construction (MuJoCo's contact reference acceleration
-# drives dist -> margin), so fp32 geometry (~1e-7 m) decides their activation on a coin toss,
-# and the Newton Hessian M + J'DJ pairs finger inertias ~1e-3 with contact stiffness ~1
-# (condition ~1e4): an fp32 solve of the same state differs from fp64 by ~cond * 1e-7 ~ 1e-3
-# relative in qacc.  The grasp tests therefore also state a solver-relative velocity tolerance,
-# |dqvel| <= 5e-3 (1 + |v|) + 2e-2 * h * frame_skip * |qacc| (qacc: the oracle's last substep),
-# which the strict tolerance above is reported beside.
-SOLVER_REL = 2e-2
+# Grasp regime (DAPG policies; hammer: fingers closed on the handle, head striking the nail):
+# the same one-step tolerance, on every (env, step) of 80-step policy rollouts.  Resting
+# contacts sit AT their margin by construction (MuJoCo's contact reference acceleration drives
+# dist -> margin), so fp32 geometry (~1e-7 m) can switch one on or off where fp64 does not:
+# those are the discrete events the thresholds leave room for.
 
 
 def _no_overflow(sim, n):
@@ -318,20 +314,15 @@ def test_determinism():
 # substep).  tools/debug_sub.py shows forward internals identical to 4e-7 relative up to that
 # substep.
 TEACHER_FORCED_MIN = {"hammer-v0": 0.995, "door-v0": 0.995, "relocate-v0": 0.995, "pen-v0": 0.995}
-# grasp regime (module comment at SOLVER_REL): strict tolerance / solver-relative tolerance /
-# rewards.  hammer: measured 0.953 / see profiles/r02_pytest_gpu.txt / 0.986 (the head strikes
-# the nail: impact accelerations ~1e3, the rest of the reward is distance terms of fingers that
-# rest at their contact margins)
-GRASP_MIN = {"hammer-v0": (0.94, 0.99), "door-v0": (0.995, 0.995), "pen-v0": (0.99, 0.995),
-             "relocate-v0": (0.995, 0.995)}
-GRASP_REWARD_MIN = {"hammer-v0": 0.98, "door-v0": 0.995, "pen-v0": 0.995, "relocate-v0": 0.995}
+GRASP_MIN = {"hammer-v0": 0.995, "door-v0": 0.995, "pen-v0": 0.99, "relocate-v0": 0.995}
 # the MPR collider forced to the other precision than the task default (tasks.py mpr_fp64):
 # pen in fp32 resolves shallow face-on-face cylinder contacts differently (~81 %, see
 # aw_collide.h namespace mpr); hammer / door in fp64
 # pen with fp32 MPR measured 0.827: its capsule phalanges lie along the cylinder (line
 # contacts), where the support points MPR picks flip on the sign of a ~0 component; the portal
 # (and the depth, ~3e-5 m apart) then follows a different path than in fp64.  The task default
-# for pen is fp64 MPR (MuJoCo's libccd precision), which passes at 0.995.
+# for pen and hammer is fp64 MPR (MuJoCo's libccd precision); hammer's fp32 path passes the
+# random-policy test at 0.995 (its face-on-face head contacts come with the DAPG grasp regime).
 TEACHER_FORCED_MIN_MPR_OTHER = {"hammer-v0": 0.995, "door-v0": 0.995, "pen-v0": 0.80}
 
 
@@ -345,9 +336,8 @@ def test_teacher_forced_trajectory(env_id):
 def test_teacher_forced_dapg_grasp(env_id):
     """Teacher forcing along DAPG-policy rollouts (grasp / manipulation regime: up to ~20
     contacts and ~100 dense rows per substep), oracle at MuJoCo's capacities, no overflow."""
-    frac, frac_rel = _teacher_forced(env_id, 0, policy=True, steps=80)
-    lo, lo_rel = GRASP_MIN[env_id]
-    assert frac >= lo and frac_rel >= lo_rel, (env_id, frac, frac_rel)
+    frac = _teacher_forced(env_id, 0, policy=True, steps=80)
+    assert frac >= GRASP_MIN[env_id], (env_id, frac)
 
 
 @pytest.mark.parametrize("env_id", sorted(TEACHER_FORCED_MIN_MPR_OTHER))
@@ -392,9 +382,8 @@ def _teacher_forced(env_id, disableflags, policy=False, steps=40):
         from conftest import GOLDEN
         from mj_envs_amd.policy import GaussianMLP
         pol = GaussianMLP.from_npz(os.path.join(GOLDEN, f"dapg_{env_id.split('-')[0]}.npz"))
-    oks, oks_rel, rok = [], [], []
+    oks, rok = [], []
     ostatus = 0
-    hstep = float(m.opt.get("timestep", 0.002)) * sim.frame_skip
     for k in range(steps):
         sim.get_state(q, v, w)
         torch.cuda.synchronize()
@@ -408,22 +397,17 @@ def _teacher_forced(env_id, disableflags, policy=False, steps=40):
         ostatus |= int(np.bitwise_or.reduce(ost))
         qg, vg = q.cpu().numpy(), v.cpu().numpy()
         okq = (np.abs(qg - st["qpos"]) <= 2e-5 + 1e-5 * np.abs(st["qpos"])).all(axis=1)
-        dv = np.abs(vg - st["qvel"])
-        okv = (dv <= 5e-3 * (1 + np.abs(st["qvel"]))).all(axis=1)
-        okv_rel = (dv <= 5e-3 * (1 + np.abs(st["qvel"])) + SOLVER_REL * hstep * np.abs(st["warm"])).all(axis=1)
+        okv = (np.abs(vg - st["qvel"]) <= 5e-3 * (1 + np.abs(st["qvel"]))).all(axis=1)
         oks.append(okq & okv)
-        oks_rel.append(okq & okv_rel)
         rok.append(_rewards_close(rew.cpu().numpy(), r_ref, check=False))
     frac = np.concatenate(oks).mean()
-    frac_rel = np.concatenate(oks_rel).mean()
     rfrac = np.concatenate(rok).mean()
     print(f"teacher-forced {env_id} (disableflags {disableflags:#x}{', DAPG policy' if policy else ''}): "
-          f"{frac:.4f} of {n * steps} (env, step) cases within the state tolerance, {frac_rel:.4f} within the "
-          f"solver-relative one, rewards {rfrac:.4f}")
+          f"{frac:.4f} of {n * steps} (env, step) cases within the state tolerance, rewards {rfrac:.4f}")
     assert not (ostatus & 24), "oracle overflowed MuJoCo's capacities"
     _no_overflow(sim, n)
-    assert rfrac >= (REWARD_MIN if not policy else GRASP_REWARD_MIN[env_id]), (env_id, rfrac)
-    return (frac, frac_rel) if policy else frac
+    assert rfrac >= REWARD_MIN, (env_id, rfrac)
+    return frac
 
 
 @pytest.mark.parametrize("variation", ["mass", "pos", "size"])

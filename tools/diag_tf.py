@@ -109,6 +109,24 @@ def main(env_id="hammer-v0", pol_kind="dapg", steps=80, n=64, max_cases=12, dsbl
                                or any(x[0] != y[0] for x, y in zip(ocs, gcs))):
                 sub["contacts_gpu"] = gcs
                 sub["contacts_oracle"] = ocs
+            if rq > 2e-3 and d["nefc"] == int(sc[1]):
+                # same rows: where does the solve part?  per-row D / aref / force, contact frames
+                ne = d["nefc"]
+                od, oa, of = o.get("efc_D"), o.get("efc_aref"), o.get("efc_force")
+                rel = lambda a, b: float(np.abs(a - b).max() / (np.abs(b).max() + 1e-12))
+                sub["rows"] = dict(D=rel(d["efc_D"][:ne], od), aref=rel(d["efc_aref"][:ne], oa),
+                                   force=rel(d["efc_force"][:ne], of),
+                                   worst_force_rows=[(int(r), int(d["efc_type"][r]), float(d["efc_force"][r]),
+                                                      float(of[r])) for r in np.argsort(-np.abs(d["efc_force"][:ne] - of))[:4]])
+                if len(oc):
+                    sub["contact_pos_err"] = float(np.abs(d["con_pos"] - oc[:, 1:4]).max())
+                    fe = np.abs(d["con_frame"] - oc[:, 4:13]).max(axis=1)
+                    sub["contact_frame_err"] = float(fe.max())
+                    sub["frame_err_by_contact"] = [(gname(m, int(c[13])) + "|" + gname(m, int(c[14])), round(float(e), 5),
+                                                    [round(float(x), 4) for x in c[4:7]])
+                                                   for c, e in zip(oc, fe) if e > 1e-4]
+                sub["qacc_smooth"] = rel(d["qacc_smooth"], o.get("qacc_smooth"))
+                sub["qM"] = rel(d["qM"], o.get("qM").reshape(len(oq), len(oq)))
             rec["substeps"].append(sub)
             o.mjstep1(pre["params"], qp, qv, wm, ctrl, 1)
             if rq > 2e-3 or "contacts_gpu" in sub:
