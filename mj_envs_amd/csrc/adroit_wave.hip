@@ -170,6 +170,9 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV], Dof& d
     chol_factor<NV>(row, lane, invd, s);
     chol_store<NV>(row, lane, s);
     wsync();
+#ifndef AW_NOSLIP_REFACTOR
+    if (s.nefc > 0 && m.noslip_iterations > 0 && !(m.disableflags & DSBL_NOSLIP)) msave_store<NV>(m, s, lane);
+#endif
     d.qacc_smooth = chol_solve<NV>(row, invd, lane < NV ? d.qfrc_smooth : 0.f, lane, s);
   }
   AW_PROF(s, PR_SMOOTH);
@@ -1040,6 +1043,7 @@ static void free_handle(aw_handle* h) {
   if (h->dmhdr) (void)hipFree(h->dmhdr);
   if (h->dstate) (void)hipFree(h->dstate);
   if (h->m.jspill) (void)hipFree(h->m.jspill);
+  if (h->m.msave) (void)hipFree(h->m.msave);
   delete h;
 }
 
@@ -1074,6 +1078,7 @@ int aw_create(const void* blob, size_t nbytes, int n_envs, int device, aw_handle
   HIPCHK(hipMemcpy(h->dmodel, md.get(), sizeof(MData), hipMemcpyHostToDevice));
   h->m.d = (const MData*)h->dmodel;
   HIPCHK(hipMalloc((void**)&h->m.jspill, (size_t)n_envs * JSPILL * sizeof(float)));
+  HIPCHK(hipMalloc((void**)&h->m.msave, (size_t)n_envs * NPACK_SAVE * sizeof(float)));
   HIPCHK(hipMalloc(&h->dmhdr, sizeof(DModel) + sizeof(DState)));
   const size_t bytes = layout_state(h.get(), nullptr);   // dry run: sizes only
   HIPCHK(hipMalloc(&h->dstate, bytes));

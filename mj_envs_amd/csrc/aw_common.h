@@ -181,6 +181,7 @@ struct DModel {
   int nrgeom;                 // rendered geoms
   const MData* __restrict__ d;
   float* jspill;              // per-env dense-J overflow rows [nenv][JSPILL] (device)
+  float* msave;               // per-env copy of the smooth solve's factor of M [nenv][NPACK_SAVE]
   unsigned long long env_offset;   // global id of env 0 of this handle (shards): Philox keys
 };
 
@@ -199,6 +200,7 @@ struct DModel {
 // 16-byte aligned tri(j), so uniform reads along a row are ds_read_b128 broadcasts
 __host__ __device__ constexpr int tri(int j) { return 4 * (j + 2 * (j / 4) * (j / 4 - 1) + (j % 4) * (j / 4)); }
 constexpr int NPACK = tri(MAXV);
+constexpr int NPACK_SAVE = ((NPACK + 255) / 256) * 256;   // 64 lanes x 16-byte chunks
 
 struct __attribute__((aligned(16))) Env {
   union {

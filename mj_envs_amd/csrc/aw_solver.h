@@ -134,6 +134,28 @@ AW_DEV void jspill_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// The smooth solve's factor of M is needed again by noslip (inv(M)) after Newton has reused the
+// LDS factor storage: it is parked in this env's global block (L2-resident, 16-byte vector
+// stores / loads, lane-dependent addresses) instead of refactoring M.
+AW_DEV float4* msave_block(const DModel& m, const Env& s) {
+  return reinterpret_cast<float4*>(m.msave + (size_t)s.env * NPACK_SAVE);
+}
+template <int NV>
+AW_DEV void msave_store(const DModel& m, const Env& s, int lane) {
+  constexpr int n4 = (tri(NV) + 3) / 4;
+  float4* dst = msave_block(m, s);
+  const float4* src = reinterpret_cast<const float4*>(s.L);
+  for (int i = lane; i < n4; i += 64) dst[i] = src[i];
+}
+template <int NV>
+AW_DEV void msave_load(const DModel& m, Env& s, int lane) {
+  constexpr int n4 = (tri(NV) + 3) / 4;
+  jspill_fence();   // the stores of msave_store (same wave) are complete
+  const float4* src = msave_block(m, s);
+  float4* dst = reinterpret_cast<float4*>(s.L);
+  for (int i = lane; i < n4; i += 64) dst[i] = src[i];
+}
+
 // J_r . x  (x in LDS); r is per lane
 template <int NV>
 AW_DEV float row_dot(const DModel& m, const Env& s, int r, const float* x) {
@@ -647,12 +669,19 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
   float Mi[NV];
   {
     float row[NV];
+#ifdef AW_NOSLIP_REFACTOR
 #pragma unroll
     for (int k = 0; k < NV; k++) row[k] = Mrow[k];
     float invd = 1.f;
     chol_factor<NV>(row, lane, invd, s);
     chol_store<NV>(row, lane, s);
     if (lane < NV) s.vec2[lane] = invd;
+#else
+    (void)row;
+    msave_load<NV>(m, s, lane);
+    wsync();
+    if (lane < NV) s.vec2[lane] = __builtin_amdgcn_rcpf(s.L[tri(lane) + lane]);
+#endif
     wsync();
   }
 #pragma unroll

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--env", default="hammer-v0")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--preroll", type=int, default=-1, help="untimed steps first (default: one horizon)")
     a = ap.parse_args()
     if a.build:
         build()
@@ -46,7 +47,11 @@ def main():
     act = sim.empty(a.envs, sim.nu)
     rew, done, goal = sim.empty(a.envs), sim.empty(a.envs, dtype=torch.uint8), sim.empty(a.envs, dtype=torch.uint8)
     sim.reset(obs, seed=1)
-    for k in range(5):
+    # the bench's steady state: staggered episode phases + one horizon of pre-roll
+    from mj_envs_amd.dist import stagger_phases
+    sim.set_episode(ep_len=torch.from_numpy(stagger_phases(a.envs, 0, sim.horizon)).cuda())
+    pre = sim.horizon if a.preroll < 0 else a.preroll
+    for k in range(pre):
         sim.random_actions(act, 0, k)
         sim.step(act, obs, rew, done, goal, autoreset=True, seed=1)
     torch.cuda.synchronize()
@@ -54,7 +59,7 @@ def main():
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     ev[0].record()
     for k in range(a.steps):
-        sim.random_actions(act, 0, 5 + k)
+        sim.random_actions(act, 0, pre + k)
         sim.step(act, obs, rew, done, goal, autoreset=True, seed=1)
     ev[1].record()
     torch.cuda.synchronize()
