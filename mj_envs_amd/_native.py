@@ -106,7 +106,8 @@ EXPORTS = ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "a
 STAGES = ("pre", "kinematics", "collision", "com_crb", "rne_smooth_solve", "constraints", "newton",
           "noslip", "jt_touch", "euler", "task_obs", "reset", "checks")
 SUBSTAGES = ("nt_init", "nt_hess", "nt_chol", "nt_solve", "nt_ls", "nt_upd", "ns_minv", "ns_setup", "ns_iter",
-             "co_broad", "co_narrow", "com", "rne", "co_plane", "co_round", "co_roundbox", "co_boxbox")
+             "co_broad", "co_narrow", "com", "rne", "co_plane", "co_round", "co_roundbox", "co_boxbox",
+             "nt_hsparse", "nt_hoffd")
 
 
 def stage_profile(reset: bool = True) -> dict:
@@ -119,6 +120,7 @@ def stage_profile(reset: bool = True) -> dict:
     out["newton_iters"], out["noslip_iters"], out["nefc"], out["ncon"] = v[15], v[16], v[17], v[18]
     for i, name in enumerate(SUBSTAGES):
         out[name] = v[19 + i]
+    out["offd_rows"] = v[38]
     return out
 
 

@@ -48,7 +48,8 @@ enum {
   PR_EULER, PR_TASK, PR_RESET, PR_CHECK, PR_CALLS, PR_SUBSTEPS,
   PR_NEWTON_IT, PR_NOSLIP_IT, PR_NEFC, PR_NCON,
   PR_NT_INIT, PR_NT_HESS, PR_NT_CHOL, PR_NT_SOLVE, PR_NT_LS, PR_NT_UPD, PR_NS_MINV, PR_NS_SETUP, PR_NS_ITER,
-  PR_CO_BROAD, PR_CO_NARROW, PR_COM, PR_RNE, PR_CO_C0, PR_CO_C1, PR_CO_C2, PR_CO_C3
+  PR_CO_BROAD, PR_CO_NARROW, PR_COM, PR_RNE, PR_CO_C0, PR_CO_C1, PR_CO_C2, PR_CO_C3,
+  PR_NT_HSPARSE, PR_NT_HOFFD, PR_NT_OFFD_ROWS
 };
 #ifdef AW_STAGE_PROF
 #define AW_PROF_START(S)                                            \

@@ -515,6 +515,7 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
       }
     }
     if (full) {
+#ifdef AW_HESS_REGOFFD
     // Hessian H = M + J' D_quad J.  Sparse rows: diagonal terms gathered through an LDS vector,
     // the off-diagonal term of a two-dof (tendon) row added in registers by the two lanes it
     // couples; dense rows: rank-1 updates with the row broadcast from LDS.
@@ -538,6 +539,7 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
       offd[h] = __ballot(od);
     }
     wsync();
+    AW_PROF(s, PR_NT_HSPARSE);
     {
       const float dg = s.hdiag[li];
 #pragma unroll
@@ -554,8 +556,56 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
         const int other = lane == i0 ? i1 : (lane == i1 ? i0 : -1);
 #pragma unroll
         for (int k = 0; k < NV; k++) H[k] += k == other ? val : 0.f;
+        AW_PROF_ADD(s, PR_NT_OFFD_ROWS, 1);
       }
     }
+#else
+    // Hessian H = M + J' D_quad J, lower triangle only (the right-looking factorisation never
+    // reads a lane's entries above its diagonal).  Sparse rows (<= 2 dofs: frictionloss, joint
+    // and tendon limits) are scattered with LDS atomics into the packed lower triangle in the
+    // factor's own storage s.L (dead until chol_store), which each lane then adds to its row
+    // with 16-byte reads -- a two-dof tendon row's off-diagonal term lands in ONE entry, where
+    // adding it in registers took a 2 x NV select chain per row.  Dense rows: rank-1 updates
+    // with the row broadcast from LDS.
+    {
+      constexpr int n4 = (tri(NV) + 3) / 4;
+      float4* Lz = reinterpret_cast<float4*>(s.L);
+      for (int i = lane; i < n4; i += 64) Lz[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    wsync();
+#pragma unroll
+    for (int h = 0; h < NRL; h++) {
+      int r = lane + 64 * h;
+      if (r < nefc) {
+        float w = rr[h].st == S_QUAD ? rr[h].D : 0.f;
+        s.rowbuf[r] = w;
+        if (r < s.nsparse && w != 0.f) {
+          int i0 = s.efc_i0[r], i1 = s.efc_i1[r];
+          float v0 = s.efc_v0[r], v1 = s.efc_v1[r];
+          atomicAdd(&s.L[tri(i0) + i0], w * v0 * v0);
+          if (i1 >= 0) {
+            atomicAdd(&s.L[tri(i1) + i1], w * v1 * v1);
+            const int hi = i0 > i1 ? i0 : i1, lo = i0 > i1 ? i1 : i0;
+            atomicAdd(&s.L[tri(hi) + lo], w * v0 * v1);
+          }
+        }
+      }
+    }
+    wsync();
+    AW_PROF(s, PR_NT_HSPARSE);
+    {
+      const float* Lr = &s.L[tri(li)];
+#pragma unroll
+      for (int q = 0; q < (NV + 3) / 4; q++) {
+        const float4 v = q * 4 <= li ? *reinterpret_cast<const float4*>(Lr + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+          if (4 * q + t < NV) H[4 * q + t] = Mrow[4 * q + t] + vv[t];
+      }
+    }
+#endif
+    AW_PROF(s, PR_NT_HOFFD);
     const int nd = s.ndense, ndl = nd < JL ? nd : JL;
     for (int d = 0; d < ndl; d++) {
       float w = s.rowbuf[s.nsparse + d];
