@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -265,7 +266,7 @@ AW_DEV void load_env(const DModel& m, Env& s, const DState& st, int env, int lan
     s.qvel[lane] = st.qvel[(size_t)env * m.nv + lane];
     s.warm[lane] = st.warm[(size_t)env * m.nv + lane];
   }
-  if (lane == 0) { s.status = 0u; s.env = env; }
+  if (lane == 0) { s.status = 0u; s.slot = blockIdx.x; }
 }
 template <int NV>
 AW_DEV void store_env(const DModel& m, Env& s, const DState& st, int env, int lane) {
@@ -329,7 +330,8 @@ template <int NV, int MP>
 __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DModel* __restrict__ mptr, DState stval,
                                              int n, const float* __restrict__ actions,
                                              float* obs, float* reward, uint8_t* done, uint8_t* goal,
-                                             float* terminal_obs, int autoreset, uint64_t seed) {
+                                             float* terminal_obs, int autoreset, uint64_t seed,
+                                             int* __restrict__ next_env) {
 #ifndef AW_MODEL_BYVAL
   // model scalars read from the device copy on demand (scalar loads behind the loop's memory
   // clobber) instead of ~50 kernel-argument SGPRs held live across the whole launch
@@ -346,88 +348,98 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
   const DState& st = stval;
 #endif
   __shared__ Env s;
-  const int env = blockIdx.x, lane = threadIdx.x;
-  if (env >= n) return;
-  AW_PROF_START(s);
-  load_env<NV>(m, s, st, env, lane);
-  if (lane < m.nu) {
-    float a = clampf(actions[(size_t)env * m.nu + lane], -1.f, 1.f);
-    s.ctrl[lane] = MD(act_mid, lane) + a * MD(act_rng, lane);
-  }
-  stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
-  float Mrow[NV];
-  Dof d;
-  float* ob = obs + (size_t)env * m.obs_dim;
-  int sub = 0;
-  bool resetting = false, retry = false;
-  AW_PROF(s, PR_PRE);
-#pragma nounroll
-  while (true) {
-    // memory clobber: keeps LICM from hoisting the (loop-invariant) model loads of a whole
-    // substep out of this loop, which would pin them in registers across every stage
-    asm volatile("" ::: "memory");
-    if (!resetting && !retry) check_state<NV>(s, lane);
-    AW_PROF(s, PR_CHECK);
-    forward<NV, MP>(m, s, lane, Mrow, d);
-    if (resetting) break;
-    if (!retry && check_acc<NV>(s, lane, d)) { retry = true; continue; }
-    retry = false;
-    euler<NV>(m, s, lane, Mrow, d);
-    AW_PROF(s, PR_EULER);
-    AW_PROF_COUNT(s, PR_SUBSTEPS);
-    if (++sub < m.frame_skip) continue;
-    // env-step complete: observation, reward, episode bookkeeping
-    write_obs(m, s, lane, ob);
-    int term = 0, trunc = 0;
-    if (lane == 0) {
-      float r;
-      int dn, gl;
-      task_reward(m, s, &r, &dn, &gl);
-      reward[env] = r;
-      goal[env] = (uint8_t)gl;
-      int t = st.ep_len[env] + 1;
-      term = dn;
-      trunc = (m.horizon > 0 && t >= m.horizon) ? 1 : 0;
-      done[env] = (uint8_t)(term | (trunc << 1));
-      float ret = st.ep_ret[env] + r;
-      int gcount = st.ep_goal[env] + gl;
-      st.ep_len[env] = t;
-      st.ep_ret[env] = ret;
-      st.ep_goal[env] = gcount;
-      st.status[env] = s.status;
-      st.status_acc[env] |= s.status;
-      if (term || trunc) {
-        st.last_ret[env] = ret;
-        st.last_goal[env] = gcount;
-        st.last_len[env] = t;
-        st.episode[env] += 1;
-        st.sum_ret[env] += ret;
-        st.n_success[env] += gcount > m.success_steps ? 1 : 0;
-      }
-    }
-    store_env<NV>(m, s, st, env, lane);
-    AW_PROF(s, PR_TASK);
-    int ended = __shfl(term | trunc, 0, 64);
-    if (!(autoreset && ended)) break;
-    __threadfence_block();
-    if (terminal_obs)
-      for (int o = lane; o < m.obs_dim; o += 64) terminal_obs[(size_t)env * m.obs_dim + o] = s.rowbuf[o];
+  const int lane = threadIdx.x;
+  // Persistent workgroups: the grid is one workgroup per resident slot (launch_step); each takes
+  // env blockIdx.x first, then the next unclaimed env from the launch's counter, so the per-slot
+  // spill / M-factor blocks (s.slot) are rewritten in the XCD's L2 instead of streaming a
+  // per-env block to memory.  Every workgroup exits once the counter passes n.
+  for (int env = blockIdx.x; env < n;) {
     wsync();
-    reset_prepare<NV>(m, s, st, env, lane, nullptr, seed);
-    AW_PROF(s, PR_RESET);
-    resetting = true;
-  }
-  if (resetting) {
-    write_obs(m, s, lane, ob);
-    store_env<NV>(m, s, st, env, lane);
-    if (lane == 0) st.status_acc[env] |= s.status;
-  }
+    AW_PROF_START(s);
+    load_env<NV>(m, s, st, env, lane);
+    if (lane < m.nu) {
+      float a = clampf(actions[(size_t)env * m.nu + lane], -1.f, 1.f);
+      s.ctrl[lane] = MD(act_mid, lane) + a * MD(act_rng, lane);
+    }
+    stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
+    float Mrow[NV];
+    Dof d;
+    float* ob = obs + (size_t)env * m.obs_dim;
+    int sub = 0;
+    bool resetting = false, retry = false;
+    AW_PROF(s, PR_PRE);
+#pragma nounroll
+    while (true) {
+      // memory clobber: keeps LICM from hoisting the (loop-invariant) model loads of a whole
+      // substep out of this loop, which would pin them in registers across every stage
+      asm volatile("" ::: "memory");
+      if (!resetting && !retry) check_state<NV>(s, lane);
+      AW_PROF(s, PR_CHECK);
+      forward<NV, MP>(m, s, lane, Mrow, d);
+      if (resetting) break;
+      if (!retry && check_acc<NV>(s, lane, d)) { retry = true; continue; }
+      retry = false;
+      euler<NV>(m, s, lane, Mrow, d);
+      AW_PROF(s, PR_EULER);
+      AW_PROF_COUNT(s, PR_SUBSTEPS);
+      if (++sub < m.frame_skip) continue;
+      // env-step complete: observation, reward, episode bookkeeping
+      write_obs(m, s, lane, ob);
+      int term = 0, trunc = 0;
+      if (lane == 0) {
+        float r;
+        int dn, gl;
+        task_reward(m, s, &r, &dn, &gl);
+        reward[env] = r;
+        goal[env] = (uint8_t)gl;
+        int t = st.ep_len[env] + 1;
+        term = dn;
+        trunc = (m.horizon > 0 && t >= m.horizon) ? 1 : 0;
+        done[env] = (uint8_t)(term | (trunc << 1));
+        float ret = st.ep_ret[env] + r;
+        int gcount = st.ep_goal[env] + gl;
+        st.ep_len[env] = t;
+        st.ep_ret[env] = ret;
+        st.ep_goal[env] = gcount;
+        st.status[env] = s.status;
+        st.status_acc[env] |= s.status;
+        if (term || trunc) {
+          st.last_ret[env] = ret;
+          st.last_goal[env] = gcount;
+          st.last_len[env] = t;
+          st.episode[env] += 1;
+          st.sum_ret[env] += ret;
+          st.n_success[env] += gcount > m.success_steps ? 1 : 0;
+        }
+      }
+      store_env<NV>(m, s, st, env, lane);
+      AW_PROF(s, PR_TASK);
+      int ended = __shfl(term | trunc, 0, 64);
+      if (!(autoreset && ended)) break;
+      __threadfence_block();
+      if (terminal_obs)
+        for (int o = lane; o < m.obs_dim; o += 64) terminal_obs[(size_t)env * m.obs_dim + o] = s.rowbuf[o];
+      wsync();
+      reset_prepare<NV>(m, s, st, env, lane, nullptr, seed);
+      AW_PROF(s, PR_RESET);
+      resetting = true;
+    }
+    if (resetting) {
+      write_obs(m, s, lane, ob);
+      store_env<NV>(m, s, st, env, lane);
+      if (lane == 0) st.status_acc[env] |= s.status;
+    }
 #ifdef AW_STAGE_PROF
-  AW_PROF(s, PR_TASK);
-  AW_PROF_COUNT(s, PR_CALLS);
-  if (lane == 0)
-    for (int i = 0; i < AW_NPROF; i++) atomicAdd(&g_stage_prof[i], s.prof_acc[i]);
+    AW_PROF(s, PR_TASK);
+    AW_PROF_COUNT(s, PR_CALLS);
+    if (lane == 0)
+      for (int i = 0; i < AW_NPROF; i++) atomicAdd(&g_stage_prof[i], s.prof_acc[i]);
 #endif
+    if ((int)gridDim.x >= n) break;            // one env per workgroup: no counter
+    int claim = 0;
+    if (lane == 0) claim = atomicAdd(next_env, 1);
+    env = (int)gridDim.x + __shfl(claim, 0, 64);
+  }
 }
 
 template <int NV, int MP>
@@ -437,7 +449,7 @@ __global__ void __launch_bounds__(64) k_reset(DModel m, DState st, int n, const 
   const int env = blockIdx.x, lane = threadIdx.x;
   if (env >= n) return;
   if (mask && !mask[env]) return;
-  if (lane == 0) { s.status = 0u; s.env = env; }
+  if (lane == 0) { s.status = 0u; s.slot = blockIdx.x; }
   reset_env<NV, MP>(m, s, st, env, lane, params, seed, obs);
   store_env<NV>(m, s, st, env, lane);
   if (lane == 0) { st.status[env] = s.status; st.status_acc[env] |= s.status; }
@@ -686,6 +698,7 @@ struct aw_handle {
   void* dmodel = nullptr;
   void* dmhdr = nullptr;   // device copy of m (k_step reads its scalars from here)
   void* dstate = nullptr;
+  int* next_env = nullptr;   // k_step's work counter (env claims past the first grid's worth)
 };
 
 static int upload_header(aw_handle* h) {
@@ -986,8 +999,20 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
 template <int NV, int MP>
 static void launch_step(aw_handle* h, const float* a, float* obs, float* rew, uint8_t* done, uint8_t* goal,
                         float* tobs, int autoreset, uint64_t seed, hipStream_t st) {
-  hipLaunchKernelGGL((k_step<NV, MP>), dim3(h->nenv), dim3(64), 0, st, h->m, (const DModel*)h->dmhdr, h->st, h->nenv, a, obs, rew, done,
-                     goal, tobs, autoreset, seed);
+  // grid = the workgroups the chip holds at once (occupancy x CUs), capped at nenv;
+  // AW_STEP_GRID=<n> overrides (0: one workgroup per env, the non-persistent launch)
+  static int slots = -1;
+  if (slots < 0) {
+    int per_cu = 0, cus = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_step<NV, MP>, 64, 0);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
+    slots = std::max(per_cu, 1) * std::max(cus, 1);
+    if (const char* e = getenv("AW_STEP_GRID")) slots = atoi(e) > 0 ? atoi(e) : 1 << 30;
+  }
+  const int grid = std::min(h->nenv, slots);
+  if (grid < h->nenv) (void)hipMemsetAsync(h->next_env, 0, sizeof(int), st);
+  hipLaunchKernelGGL((k_step<NV, MP>), dim3(grid), dim3(64), 0, st, h->m, (const DModel*)h->dmhdr, h->st, h->nenv, a, obs, rew, done,
+                     goal, tobs, autoreset, seed, h->next_env);
 }
 template <int NV, int MP>
 static void launch_reset(aw_handle* h, const uint8_t* mask, const float* params, uint64_t seed, float* obs,
@@ -1044,6 +1069,7 @@ static void free_handle(aw_handle* h) {
   if (h->dstate) (void)hipFree(h->dstate);
   if (h->m.jspill) (void)hipFree(h->m.jspill);
   if (h->m.msave) (void)hipFree(h->m.msave);
+  if (h->next_env) (void)hipFree(h->next_env);
   delete h;
 }
 
@@ -1080,6 +1106,7 @@ int aw_create(const void* blob, size_t nbytes, int n_envs, int device, aw_handle
   HIPCHK(hipMalloc((void**)&h->m.jspill, (size_t)n_envs * JSPILL * sizeof(float)));
   HIPCHK(hipMalloc((void**)&h->m.msave, (size_t)n_envs * NPACK_SAVE * sizeof(float)));
   HIPCHK(hipMalloc(&h->dmhdr, sizeof(DModel) + sizeof(DState)));
+  HIPCHK(hipMalloc((void**)&h->next_env, sizeof(int)));
   const size_t bytes = layout_state(h.get(), nullptr);   // dry run: sizes only
   HIPCHK(hipMalloc(&h->dstate, bytes));
   HIPCHK(hipMemset(h->dstate, 0, bytes));

@@ -243,7 +243,8 @@ struct __attribute__((aligned(16))) Env {
   float J[JL][VS] __attribute__((aligned(16)));
   float rowbuf[MAXEFC];
   unsigned status;
-  int env;                    // env index (selects the dense-J spill block)
+  int slot;                   // workgroup slot: selects the dense-J spill and M-factor blocks,
+                              // reused by every env the persistent k_step workgroup processes
   int it_newton, it_noslip;   // iterations of the last solve (introspection)
 #ifdef AW_STAGE_PROF
   unsigned long long prof_acc[AW_NPROF];

@@ -122,7 +122,7 @@ AW_DEV float getimpedance(const float* solimp, float pm) {
 // below uses a lane-dependent address (a row per lane, or the row's entry per lane followed by
 // a readlane broadcast), so no uniform (scalar-cache) load can see a previous substep's row.
 AW_DEV float* jspill_row(const DModel& m, const Env& s, int d) {
-  return m.jspill + (size_t)s.env * JSPILL + (size_t)(d - JL) * VS;
+  return m.jspill + (size_t)s.slot * JSPILL + (size_t)(d - JL) * VS;
 }
 AW_DEV void jput(const DModel& m, Env& s, int d, int k, float v) {
   if (d < JL) s.J[d][k] = v;
@@ -138,7 +138,7 @@ AW_DEV void jspill_fence() {
 // LDS factor storage: it is parked in this env's global block (L2-resident, 16-byte vector
 // stores / loads, lane-dependent addresses) instead of refactoring M.
 AW_DEV float4* msave_block(const DModel& m, const Env& s) {
-  return reinterpret_cast<float4*>(m.msave + (size_t)s.env * NPACK_SAVE);
+  return reinterpret_cast<float4*>(m.msave + (size_t)s.slot * NPACK_SAVE);
 }
 template <int NV>
 AW_DEV void msave_store(const DModel& m, const Env& s, int lane) {
