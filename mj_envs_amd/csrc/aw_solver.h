@@ -38,6 +38,59 @@ AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
     for (int k = j + 1; k < NV; k++) row[k] = fmaf(-lij, rlane(lij, k), row[k]);
   }
 }
+#elif defined(AW_CHOL_BLOCK4)
+// Variant: right-looking in blocks of four columns.  The 4x4 diagonal block is read with
+// v_readlane and factored uniformly on every lane; each lane then solves its own row of the
+// panel (the in-block part of the per-column updates, same fmaf order) and publishes it with ONE
+// 16-byte store straight into the packed factor s.L[tri(i) + j] -- its final place, so no
+// chol_store pass -- and the trailing rows pull four columns per 16-byte broadcast read: one LDS
+// round trip per four columns instead of per column.  Bitwise identical to the per-column form.
+#ifndef AW_CHOL_GROUP
+#define AW_CHOL_GROUP 8
+#endif
+template <int NV>
+AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
+#pragma unroll
+  for (int j = 0; j < NV; j += 4) {
+    constexpr int B4 = 4;
+    const int B = NV - j < B4 ? NV - j : B4;
+    float L4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      if (c >= B) break;
+      // in-block column: pivot and column entries broadcast through SGPRs (v_readlane)
+      const float djj = fmaxf(rlane(row[j + c], j + c), MINVAL);
+      const float inv = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
+                            __builtin_bit_cast(int, __builtin_amdgcn_rsqf(djj))));
+      L4[c] = lane == j + c ? djj * inv : row[j + c] * inv;
+      if (lane == j + c) invd = inv;
+      row[j + c] = L4[c];
+#pragma unroll
+      for (int c2 = 0; c2 < 4; c2++) {
+        if (c2 <= c || c2 >= B) continue;
+        row[j + c2] = fmaf(-L4[c], rlane(L4[c], j + c2), row[j + c2]);
+      }
+    }
+    if (lane >= j && lane < NV)
+      *reinterpret_cast<float4*>(&s.L[tri(lane) + j]) = make_float4(L4[0], L4[1], L4[2], L4[3]);
+    if (j + 4 < NV) {
+      wsync();
+#pragma unroll
+      for (int k = j + 4; k < NV; k++) {
+        // at most AW_CHOL_GROUP 16-byte reads in flight: hoisting all of them spills
+        if (((k - j - 4) % AW_CHOL_GROUP) == 0) asm volatile("" ::: "memory");
+        const float4 v = *reinterpret_cast<const float4*>(&s.L[tri(k) + j]);
+        float r = row[k];
+        r = fmaf(-L4[0], v.x, r);
+        if (B > 1) r = fmaf(-L4[1], v.y, r);
+        if (B > 2) r = fmaf(-L4[2], v.z, r);
+        if (B > 3) r = fmaf(-L4[3], v.w, r);
+        row[k] = r;
+      }
+      wsync();
+    }
+  }
+}
 #else
 template <int NV>
 AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
@@ -70,6 +123,9 @@ AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
 #endif
 template <int NV>
 AW_DEV void chol_store(const float (&row)[NV], int lane, Env& s) {
+#if defined(AW_CHOL_BLOCK4) && !defined(AW_CHOL_KEEPSTORE)
+  return;   // the blocked factorisation stores every row chunk in place
+#endif
   if (lane < NV) {
 #pragma unroll
     for (int k = 0; k < NV; k++)
@@ -87,6 +143,9 @@ AW_DEV float chol_solve(const float (&row)[NV], float invd, float b, int lane, c
   }
 #pragma unroll
   for (int j = NV - 1; j >= 0; j--) {
+#ifdef AW_SOLVE_GROUP
+    if (((NV - 1 - j) % AW_SOLVE_GROUP) == 0) asm volatile("" ::: "memory");   // bounded load hoisting
+#endif
     float xj = rlane(b, j) * rlane(invd, j);
     if (lane == j) b = xj;
     else if (lane < j) b = fmaf(-s.L[tri(j) + lane], xj, b);
@@ -423,6 +482,77 @@ AW_DEV float row_eval(const RowR& r, float jar, float* force, int* st) {
   *force = 0.f; *st = S_SAT; return 0.f;
 }
 
+#ifdef AW_HESS_MFMA
+// J_d' diag(w) J_d over the dense rows (weights w_d in s.rowbuf[nsparse + d], 0 for rows outside
+// the quadratic zone) written into the packed lower triangle s.L.  v_mfma_f32_16x16x4_f32 takes
+// four rows per K-step: lane l supplies A[i = l&15][k = l>>4] = w_d J[d][16 ti + i] and
+// B[k][j = l&15] = J[d][16 tj + j] with d = d0 + (l>>4); accumulator register r of lane l is
+// entry (16 ti + 4 (l>>4) + r, 16 tj + (l&15)).  Tiles (0,0), (1,0), (1,1) cover rows < 32;
+// columns >= 32 (hammer 33, relocate 36) are accumulated on the VALU, lane = row, and rows >= 32
+// take their entries left of column 32 from lanes < 32 by symmetry.
+template <int NV>
+AW_DEV void hess_dense_mfma(const DModel& m, Env& s, int lane) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  constexpr int NX = NV > 32 ? NV - 32 : 0;
+  const int nd = s.ndense, ns = s.nsparse;
+  const int sub = lane >> 4, col = lane & 15;
+  const int li = lane < NV ? lane : NV - 1;
+  f4 c00 = {0.f, 0.f, 0.f, 0.f}, c10 = c00, c11 = c00;
+  float hx[NX > 0 ? NX : 1];
+#pragma unroll
+  for (int k = 0; k < NX; k++) hx[k] = 0.f;
+  for (int d0 = 0; d0 < nd; d0 += 4) {
+    const int d = d0 + sub;
+    const float w = d < nd ? s.rowbuf[ns + d] : 0.f;
+    if (__ballot(w != 0.f) == 0ull) continue;
+    const int dd = d < nd ? d : nd - 1;
+    // JL is a multiple of 4: a K-step's rows are all in LDS or all in the spill block
+    const float* Jr = d0 < JL ? &s.J[dd][0] : jspill_row(m, s, dd);
+    float b0 = Jr[col], b1 = Jr[16 + col];
+    b0 = w != 0.f ? b0 : 0.f;
+    b1 = (w != 0.f && 16 + col < NV) ? b1 : 0.f;
+    c00 = __builtin_amdgcn_mfma_f32_16x16x4f32(w * b0, b0, c00, 0, 0, 0);
+    c10 = __builtin_amdgcn_mfma_f32_16x16x4f32(w * b1, b0, c10, 0, 0, 0);
+    c11 = __builtin_amdgcn_mfma_f32_16x16x4f32(w * b1, b1, c11, 0, 0, 0);
+    if (NX > 0) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int dq = d0 + q;
+        if (dq >= nd) break;
+        const float wq = s.rowbuf[ns + dq];
+        if (wq == 0.f) continue;
+        const float* Jq = d0 < JL ? &s.J[dq][0] : jspill_row(m, s, dq);
+        const float jl = Jq[li];
+        const float av = wq * jl;
+#pragma unroll
+        for (int k = 0; k < NX; k++) hx[k] = fmaf(av, rlane(jl, 32 + k), hx[k]);
+      }
+    }
+  }
+  // lower triangle + row padding (entries j <= (i | 3)) of rows < 32 from the tiles
+  auto put = [&](const f4& c, int ti, int tj) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int i = 16 * ti + 4 * sub + r, j = 16 * tj + col;
+      if (i < NV && j <= (i | 3)) s.L[tri(i) + j] = c[r];
+    }
+  };
+  put(c00, 0, 0);
+  put(c10, 1, 0);
+  put(c11, 1, 1);
+  if (NX > 0) {
+    if (lane < 32) {
+#pragma unroll
+      for (int k = 0; k < NX; k++) s.L[tri(32 + k) + lane] = hx[k];   // H[32+k][lane] = H[lane][32+k]
+    } else if (lane < NV) {
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (32 + k <= (lane | 3)) s.L[tri(lane) + 32 + k] = k < NX ? hx[k < NX ? k : 0] : 0.f;
+    }
+  }
+}
+#endif
+
 template <int NV>
 AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[NV], float& a, float qfrc_smooth,
                          float qacc_smooth) {
@@ -567,18 +697,36 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
     // with 16-byte reads -- a two-dof tendon row's off-diagonal term lands in ONE entry, where
     // adding it in registers took a 2 x NV select chain per row.  Dense rows: rank-1 updates
     // with the row broadcast from LDS.
+#ifdef AW_HESS_MFMA
+    // Dense part J_d' D J_d on the matrix cores (v_mfma_f32_16x16x4_f32, exact fp32): four dense
+    // rows per MFMA K-step into the lower 16x16 tiles of the leading 32x32 block; columns >= 32
+    // (NV > 32) on the VALU with the lane holding the row.  Every lower-triangle entry (and the
+    // row padding) of s.L is written by exactly one plain store, then the sparse rows are added
+    // with LDS atomics as below.
+#pragma unroll
+    for (int h = 0; h < NRL; h++) {
+      int r = lane + 64 * h;
+      if (r < nefc) s.rowbuf[r] = rr[h].st == S_QUAD ? rr[h].D : 0.f;
+    }
+    wsync();
+    hess_dense_mfma<NV>(m, s, lane);
+    wsync();
+#else
     {
       constexpr int n4 = (tri(NV) + 3) / 4;
       float4* Lz = reinterpret_cast<float4*>(s.L);
       for (int i = lane; i < n4; i += 64) Lz[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     wsync();
+#endif
 #pragma unroll
     for (int h = 0; h < NRL; h++) {
       int r = lane + 64 * h;
       if (r < nefc) {
         float w = rr[h].st == S_QUAD ? rr[h].D : 0.f;
+#ifndef AW_HESS_MFMA
         s.rowbuf[r] = w;
+#endif
         if (r < s.nsparse && w != 0.f) {
           int i0 = s.efc_i0[r], i1 = s.efc_i1[r];
           float v0 = s.efc_v0[r], v1 = s.efc_v1[r];
@@ -606,6 +754,7 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
     }
 #endif
     AW_PROF(s, PR_NT_HOFFD);
+#ifndef AW_HESS_MFMA
     const int nd = s.ndense, ndl = nd < JL ? nd : JL;
     for (int d = 0; d < ndl; d++) {
       float w = s.rowbuf[s.nsparse + d];
@@ -626,6 +775,7 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
         for (int k = 0; k < NV; k++) H[k] = fmaf(av, rlane(jl, k), H[k]);
       }
     }
+#endif
     wsync();
     AW_PROF(s, PR_NT_HESS);
     chol_factor<NV>(H, lane, invd, s);

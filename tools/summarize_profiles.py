@@ -43,7 +43,8 @@ def main(tag):
     write, _ = pmc(os.path.join(src, "pmc_write", "pw_counter_collection.csv"), "WRITE_SIZE")
     # calibration kernel on the same box: k_random_actions writes exactly n*nu*4 bytes
     cal, _ = pmc(os.path.join(src, "pmc_write", "pw_counter_collection.csv"), "WRITE_SIZE", "k_random_actions")
-    envs = meta["grid"] // meta["wg"]
+    # persistent k_step workgroups: the grid is the resident-slot count, not the env count
+    envs = b["config"].get("envs_per_gpu", meta["grid"] // meta["wg"])
     fetch_b = statistics.mean(fetch) * 1024
     write_b = statistics.mean(write) * 1024
     nu = 26 if "hammer" in b["config"]["workload"] else None
