@@ -38,59 +38,6 @@ AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
     for (int k = j + 1; k < NV; k++) row[k] = fmaf(-lij, rlane(lij, k), row[k]);
   }
 }
-#elif defined(AW_CHOL_BLOCK4)
-// Variant: right-looking in blocks of four columns.  The 4x4 diagonal block is read with
-// v_readlane and factored uniformly on every lane; each lane then solves its own row of the
-// panel (the in-block part of the per-column updates, same fmaf order) and publishes it with ONE
-// 16-byte store straight into the packed factor s.L[tri(i) + j] -- its final place, so no
-// chol_store pass -- and the trailing rows pull four columns per 16-byte broadcast read: one LDS
-// round trip per four columns instead of per column.  Bitwise identical to the per-column form.
-#ifndef AW_CHOL_GROUP
-#define AW_CHOL_GROUP 8
-#endif
-template <int NV>
-AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
-#pragma unroll
-  for (int j = 0; j < NV; j += 4) {
-    constexpr int B4 = 4;
-    const int B = NV - j < B4 ? NV - j : B4;
-    float L4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      if (c >= B) break;
-      // in-block column: pivot and column entries broadcast through SGPRs (v_readlane)
-      const float djj = fmaxf(rlane(row[j + c], j + c), MINVAL);
-      const float inv = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
-                            __builtin_bit_cast(int, __builtin_amdgcn_rsqf(djj))));
-      L4[c] = lane == j + c ? djj * inv : row[j + c] * inv;
-      if (lane == j + c) invd = inv;
-      row[j + c] = L4[c];
-#pragma unroll
-      for (int c2 = 0; c2 < 4; c2++) {
-        if (c2 <= c || c2 >= B) continue;
-        row[j + c2] = fmaf(-L4[c], rlane(L4[c], j + c2), row[j + c2]);
-      }
-    }
-    if (lane >= j && lane < NV)
-      *reinterpret_cast<float4*>(&s.L[tri(lane) + j]) = make_float4(L4[0], L4[1], L4[2], L4[3]);
-    if (j + 4 < NV) {
-      wsync();
-#pragma unroll
-      for (int k = j + 4; k < NV; k++) {
-        // at most AW_CHOL_GROUP 16-byte reads in flight: hoisting all of them spills
-        if (((k - j - 4) % AW_CHOL_GROUP) == 0) asm volatile("" ::: "memory");
-        const float4 v = *reinterpret_cast<const float4*>(&s.L[tri(k) + j]);
-        float r = row[k];
-        r = fmaf(-L4[0], v.x, r);
-        if (B > 1) r = fmaf(-L4[1], v.y, r);
-        if (B > 2) r = fmaf(-L4[2], v.z, r);
-        if (B > 3) r = fmaf(-L4[3], v.w, r);
-        row[k] = r;
-      }
-      wsync();
-    }
-  }
-}
 #else
 template <int NV>
 AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
@@ -123,9 +70,6 @@ AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
 #endif
 template <int NV>
 AW_DEV void chol_store(const float (&row)[NV], int lane, Env& s) {
-#if defined(AW_CHOL_BLOCK4) && !defined(AW_CHOL_KEEPSTORE)
-  return;   // the blocked factorisation stores every row chunk in place
-#endif
   if (lane < NV) {
 #pragma unroll
     for (int k = 0; k < NV; k++)
@@ -143,9 +87,6 @@ AW_DEV float chol_solve(const float (&row)[NV], float invd, float b, int lane, c
   }
 #pragma unroll
   for (int j = NV - 1; j >= 0; j--) {
-#ifdef AW_SOLVE_GROUP
-    if (((NV - 1 - j) % AW_SOLVE_GROUP) == 0) asm volatile("" ::: "memory");   // bounded load hoisting
-#endif
     float xj = rlane(b, j) * rlane(invd, j);
     if (lane == j) b = xj;
     else if (lane < j) b = fmaf(-s.L[tri(j) + lane], xj, b);
