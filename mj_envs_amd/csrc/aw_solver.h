@@ -405,7 +405,24 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
 // ---------------------------------------------------------------------------------------
 // Newton solver
 constexpr float GRAD_NOISE = 2e-6f;   // ~16 fp32 ulps of the gradient's terms
-constexpr int NSP_CACHE = 8;          // noslip edge pairs whose J / X rows stay in VGPRs
+#ifndef AW_NSP_CACHE
+#define AW_NSP_CACHE 12
+#endif
+constexpr int NSP_CACHE = AW_NSP_CACHE;   // noslip edge pairs whose J / X rows stay in VGPRs
+// noslip edge pairs past the VGPR cache park their X rows (inv(M) J_e', two dof vectors: only
+// lanes < MAXV carry them, 2 * MAXV floats per pair) in LDS that is dead during the PGS sweeps:
+// the phase-K / phase-S union at the start of Env (the factor of M was consumed by inv(M)),
+// then efc_D and rowbuf (written again only after noslip).  (Parking the J rows of spilled
+// pairs as well measured slower: fewer X rows fit.)
+constexpr int XPS = 2 * MAXV;
+constexpr int NSP_UNION = (int)(offsetof(Env, qpos) / (XPS * sizeof(float)));
+constexpr int NSP_ROWS = MAXEFC / XPS;          // slots in each of efc_D and rowbuf
+constexpr int NSP_LDS = NSP_UNION + 2 * NSP_ROWS;
+AW_DEV float* xpark_slot(Env& s, int q) {
+  if (q < NSP_UNION) return reinterpret_cast<float*>(&s) + q * XPS;
+  q -= NSP_UNION;
+  return q < NSP_ROWS ? s.efc_D + q * XPS : s.rowbuf + (q - NSP_ROWS) * XPS;
+}
 struct RowR {
   float D, floss, Jaref, Jp, force;
   int st, fr, valid;
@@ -925,6 +942,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
   };
   // dense-row force of row e (uniform) / its update
   auto fd_get = [&](int e) { return e < 64 ? rlane(fd, e) : rlane(fd_hi, e - 64); };
+  auto jval = [&](int d) { return lm * (d < JL ? s.J[d][li] : jspill_row(m, s, d)[li]); };
   for (int e = 0; e + 1 < ndense; e++) {
     if (!(s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1)) continue;
     float j1, j2, x1, x2;
@@ -940,6 +958,13 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
 #pragma unroll
     for (int q = 0; q < NSP_CACHE; q++)
       if (q == p) { c_j1[q] = j1; c_j2[q] = j2; c_x1[q] = x1; c_x2[q] = x2; }
+#ifndef AW_NOSLIP_NOLDS
+    if (p >= NSP_CACHE && p < NSP_CACHE + NSP_LDS && lane < MAXV) {
+      float* slot = xpark_slot(s, p - NSP_CACHE);
+      slot[lane] = x1;
+      slot[MAXV + lane] = x2;
+    }
+#endif
   }
   wsync();
   AW_PROF(s, PR_NS_SETUP);
@@ -1003,7 +1028,17 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
       if (p < npr) pair_step(p, c_j1[p], c_j2[p], c_x1[p], c_x2[p]);
     for (int p = NSP_CACHE; p < npr; p++) {
       float j1, j2, x1, x2;
-      edge_rows(rlane_i(pr_e, p), j1, j2, x1, x2);
+      const int e = rlane_i(pr_e, p);
+#ifndef AW_NOSLIP_NOLDS
+      if (p < NSP_CACHE + NSP_LDS) {   // X rows parked in LDS, J rows from LDS / the spill block
+        const float* slot = xpark_slot(s, p - NSP_CACHE);
+        j1 = jval(e);
+        j2 = jval(e + 1);
+        x1 = lane < MAXV ? slot[lane] : 0.f;
+        x2 = lane < MAXV ? slot[MAXV + lane] : 0.f;
+      } else
+#endif
+        edge_rows(e, j1, j2, x1, x2);
       pair_step(p, j1, j2, x1, x2);
     }
     if (impr * scale < m.noslip_tolerance) break;
