@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--env", default="hammer-v0")
     ap.add_argument("--out", default=None)
     ap.add_argument("--preroll", type=int, default=-1, help="untimed steps first (default: one horizon)")
+    ap.add_argument("--policy", choices=("random", "dapg"), default="random",
+                    help="actions: Philox U(-1,1) (the bench), or the reference's pretrained DAPG policy "
+                         "(mean action, grasp regime)")
     a = ap.parse_args()
     if a.build:
         build()
@@ -51,15 +54,26 @@ def main():
     from mj_envs_amd.dist import stagger_phases
     sim.set_episode(ep_len=torch.from_numpy(stagger_phases(a.envs, 0, sim.horizon)).cuda())
     pre = sim.horizon if a.preroll < 0 else a.preroll
+    pol = None
+    if a.policy == "dapg":
+        from mj_envs_amd.policy import GaussianMLP
+        pol = GaussianMLP.from_npz(os.path.join(REPO, "tests", "golden", f"dapg_{a.env.split('-')[0]}.npz"))
+
+    def actions(k):
+        if pol is not None:
+            pol.act(obs, out=act)
+        else:
+            sim.random_actions(act, 0, k)
+
     for k in range(pre):
-        sim.random_actions(act, 0, k)
+        actions(k)
         sim.step(act, obs, rew, done, goal, autoreset=True, seed=1)
     torch.cuda.synchronize()
     _native.stage_profile(reset=True)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     ev[0].record()
     for k in range(a.steps):
-        sim.random_actions(act, 0, pre + k)
+        actions(pre + k)
         sim.step(act, obs, rew, done, goal, autoreset=True, seed=1)
     ev[1].record()
     torch.cuda.synchronize()
@@ -70,7 +84,7 @@ def main():
     tot = sum(p[k] for k in names)
     rows = {k: dict(cycles_per_wave_substep=round(p[k] / sub, 1), frac=round(p[k] / max(tot, 1), 4))
             for k in names}
-    res = dict(env=a.env, envs=a.envs, steps=a.steps, ms_per_step=round(ms, 3), waves=p["waves"],
+    res = dict(env=a.env, policy=a.policy, envs=a.envs, steps=a.steps, ms_per_step=round(ms, 3), waves=p["waves"],
                substeps=p["substeps"], cycles_per_wave_substep=round(tot / sub, 1), stages=rows,
                avg_newton_iters_per_solve=round(p["newton_iters"] / sub, 3),
                avg_noslip_iters_per_substep=round(p["noslip_iters"] / sub, 3),
