@@ -406,14 +406,13 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
 // Newton solver
 constexpr float GRAD_NOISE = 2e-6f;   // ~16 fp32 ulps of the gradient's terms
 #ifndef AW_NSP_CACHE
-#define AW_NSP_CACHE 12
+#define AW_NSP_CACHE 16
 #endif
-constexpr int NSP_CACHE = AW_NSP_CACHE;   // noslip edge pairs whose J / X rows stay in VGPRs
-// noslip edge pairs past the VGPR cache park their X rows (inv(M) J_e', two dof vectors: only
-// lanes < MAXV carry them, 2 * MAXV floats per pair) in LDS that is dead during the PGS sweeps:
-// the phase-K / phase-S union at the start of Env (the factor of M was consumed by inv(M)),
-// then efc_D and rowbuf (written again only after noslip).  (Parking the J rows of spilled
-// pairs as well measured slower: fewer X rows fit.)
+constexpr int NSP_CACHE = AW_NSP_CACHE;   // noslip edge pairs whose jd / xd rows stay in VGPRs
+// noslip edge pairs past the VGPR cache park their rows (jd = J_e - J_e+1 and xd = inv(M) jd', two
+// dof vectors: only lanes < MAXV carry them, 2 * MAXV floats per pair) in LDS that is dead during
+// the PGS sweeps: the phase-K / phase-S union at the start of Env (the factor of M was consumed
+// by inv(M)), then efc_D and rowbuf (written again only after noslip).
 constexpr int XPS = 2 * MAXV;
 constexpr int NSP_UNION = (int)(offsetof(Env, qpos) / (XPS * sizeof(float)));
 constexpr int NSP_ROWS = MAXEFC / XPS;          // slots in each of efc_D and rowbuf
@@ -904,65 +903,55 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
   if (lane + 64 < ndense) fd_hi = s.efc_force[nsparse + 64 + lane];
   qacc = lane < NV ? qacc : 0.f;
   const float scale = 1.f / (m.meaninertia * (float)(NV > 1 ? NV : 1));
-  // opposing pyramid-edge pairs (e, e+1) in row order: x = inv(M) J_e' in registers, pair
-  // constants A11, A22, A12 by wave sums; pairs with K >= MINVAL are compacted, pair p's
-  // constants in lane p, the J / x rows of the first NSP_CACHE pairs kept in VGPRs
+  // opposing pyramid-edge pairs (e, e+1) in row order.  A pair's update keeps f1 + f2 (the
+  // normal force) and moves x = f1 - f2, so d2 = -d1 and everything it needs is the difference
+  // of its two rows: jd = J_e - J_e+1 and xd = inv(M) jd' (dof vectors), K = jd . xd,
+  // r1 - r2 = jd . qacc - (aref_e - aref_e+1).  Pairs with K >= MINVAL are compacted, pair p's
+  // constants in lane p; jd / xd of the first NSP_CACHE pairs stay in VGPRs, the next NSP_LDS
+  // are parked in dead LDS, the rest are rebuilt each sweep.
   int npr = 0, pr_e = 0;
-  float pr_a11 = 0.f, pr_a22 = 0.f, pr_a12 = 0.f, pr_ik = 0.f, pr_ar1 = 0.f, pr_ar2 = 0.f;
-  float c_j1[NSP_CACHE], c_j2[NSP_CACHE], c_x1[NSP_CACHE], c_x2[NSP_CACHE];
+  float pr_k = 0.f, pr_ik = 0.f, pr_ard = 0.f;
+  float c_jd[NSP_CACHE], c_xd[NSP_CACHE];
 #pragma unroll
-  for (int p = 0; p < NSP_CACHE; p++) c_j1[p] = c_j2[p] = c_x1[p] = c_x2[p] = 0.f;
-  // J row d at this lane's dof, and (inv(M) J_d')_lane
-  auto jrow_x = [&](int d, float& jv, float& xv) {
-    float a = 0.f;
-    if (d < JL) {
-      jv = lm * s.J[d][li];
-#pragma unroll
-      for (int j = 0; j < NV; j++) a = fmaf(Mi[j], s.J[d][j], a);
-    } else {
-      const float jl = jspill_row(m, s, d)[li];
-      jv = lm * jl;
-#pragma unroll
-      for (int j = 0; j < NV; j++) a = fmaf(Mi[j], rlane(jl, j), a);
-    }
-    xv = a;
-  };
-  auto edge_rows = [&](int e, float& j1, float& j2, float& x1, float& x2) {
-    if (e + 1 < JL) {
-      j1 = lm * s.J[e][li];
-      j2 = lm * s.J[e + 1][li];
-      float a1 = 0.f, a2 = 0.f;
-#pragma unroll
-      for (int j = 0; j < NV; j++) { a1 = fmaf(Mi[j], s.J[e][j], a1); a2 = fmaf(Mi[j], s.J[e + 1][j], a2); }
-      x1 = a1; x2 = a2;
-    } else {
-      jrow_x(e, j1, x1);
-      jrow_x(e + 1, j2, x2);
-    }
-  };
-  // dense-row force of row e (uniform) / its update
-  auto fd_get = [&](int e) { return e < 64 ? rlane(fd, e) : rlane(fd_hi, e - 64); };
+  for (int p = 0; p < NSP_CACHE; p++) c_jd[p] = c_xd[p] = 0.f;
+  // J row d at this lane's dof
   auto jval = [&](int d) { return lm * (d < JL ? s.J[d][li] : jspill_row(m, s, d)[li]); };
+  // jd at this lane's dof and (inv(M) jd')_lane for the pair (e, e+1)
+  auto pair_rows = [&](int e, float& jd, float& xd) {
+    float a = 0.f;
+    if (e + 1 < JL) {
+#pragma unroll
+      for (int j = 0; j < NV; j++) a = fmaf(Mi[j], s.J[e][j] - s.J[e + 1][j], a);
+      jd = lm * (s.J[e][li] - s.J[e + 1][li]);
+    } else {
+      const float dl = jval(e) - jval(e + 1);
+#pragma unroll
+      for (int j = 0; j < NV; j++) a = fmaf(Mi[j], rlane(dl, j), a);
+      jd = dl;
+    }
+    xd = a;
+  };
+  // dense-row force of row e (uniform)
+  auto fd_get = [&](int e) { return e < 64 ? rlane(fd, e) : rlane(fd_hi, e - 64); };
   for (int e = 0; e + 1 < ndense; e++) {
     if (!(s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1)) continue;
-    float j1, j2, x1, x2;
-    edge_rows(e, j1, j2, x1, x2);
-    const float a11 = wave_sum(j1 * x1), a22 = wave_sum(j2 * x2), a12 = wave_sum(j1 * x2);
-    const float K = a11 + a22 - 2.f * a12;
+    float jd, xd;
+    pair_rows(e, jd, xd);
+    const float K = wave_sum(jd * xd);
     if (!(K >= MINVAL)) continue;
     const int p = npr++;
     if (lane == p) {
-      pr_e = e; pr_a11 = a11; pr_a22 = a22; pr_a12 = a12; pr_ik = 1.0f / K;
-      pr_ar1 = s.efc_aref[nsparse + e]; pr_ar2 = s.efc_aref[nsparse + e + 1];
+      pr_e = e; pr_k = K; pr_ik = 1.0f / K;
+      pr_ard = s.efc_aref[nsparse + e] - s.efc_aref[nsparse + e + 1];
     }
 #pragma unroll
     for (int q = 0; q < NSP_CACHE; q++)
-      if (q == p) { c_j1[q] = j1; c_j2[q] = j2; c_x1[q] = x1; c_x2[q] = x2; }
+      if (q == p) { c_jd[q] = jd; c_xd[q] = xd; }
 #ifndef AW_NOSLIP_NOLDS
     if (p >= NSP_CACHE && p < NSP_CACHE + NSP_LDS && lane < MAXV) {
       float* slot = xpark_slot(s, p - NSP_CACHE);
-      slot[lane] = x1;
-      slot[MAXV + lane] = x2;
+      slot[lane] = jd;
+      slot[MAXV + lane] = xd;
     }
 #endif
   }
@@ -1006,40 +995,42 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
     }
 #endif
     impr -= wave_sum(imp_l);
-    // opposing pyramid-edge pairs, in row order (branch-free: a zero update is an exact no-op)
-    auto pair_step = [&](int p, float j1, float j2, float x1, float x2) {
+    // opposing pyramid-edge pairs, in row order (branch-free: a zero update is an exact no-op).
+    // One wave reduction per pair on the qacc chain (r1 - r2); d2 = -d1, so the improvement is
+    // (r1 - r2) d1 + K d1^2 / 2 and qacc moves along xd.
+    auto pair_step = [&](int p, float jd, float xd) {
       const int e = rlane_i(pr_e, p);
-      const float A11 = rlane(pr_a11, p), A22 = rlane(pr_a22, p), A12 = rlane(pr_a12, p);
-      const float r1 = wave_sum(j1 * qacc) - rlane(pr_ar1, p);
-      const float r2 = wave_sum(j2 * qacc) - rlane(pr_ar2, p);
+      const float rd = wave_sum(jd * qacc) - rlane(pr_ard, p);
       const float f1 = fd_get(e), f2 = fd_get(e + 1);
       const float sum = f1 + f2, x = f1 - f2;
-      const float xn = clampf(x - 2.f * (r1 - r2) * rlane(pr_ik, p), -sum, sum);
-      const float d1 = 0.5f * (sum + xn) - f1, d2 = 0.5f * (sum - xn) - f2;
-      impr -= r1 * d1 + r2 * d2 + 0.5f * (A11 * d1 * d1 + 2.f * A12 * d1 * d2 + A22 * d2 * d2);
-      qacc = fmaf(x1, d1, fmaf(x2, d2, qacc));
-      if (lane == e) fd = f1 + d1;
-      if (lane == e + 1) fd = f2 + d2;
-      if (lane + 64 == e) fd_hi = f1 + d1;
-      if (lane + 64 == e + 1) fd_hi = f2 + d2;
+      const float xn = clampf(x - 2.f * rd * rlane(pr_ik, p), -sum, sum);
+      const float f1n = 0.5f * (sum + xn), f2n = 0.5f * (sum - xn);
+      const float d1 = f1n - f1;
+      impr -= rd * d1 + 0.5f * rlane(pr_k, p) * d1 * d1;
+      qacc = fmaf(xd, d1, qacc);
+      if (e < 64) {
+        if (lane == e) fd = f1n;
+        if (lane == e + 1) fd = f2n;       // e + 1 == 64 lands in no lane of fd ...
+        if (e == 63 && lane == 0) fd_hi = f2n;   // ... but in lane 0 of fd_hi
+      } else {
+        if (lane + 64 == e) fd_hi = f1n;
+        if (lane + 64 == e + 1) fd_hi = f2n;
+      }
     };
 #pragma unroll
     for (int p = 0; p < NSP_CACHE; p++)
-      if (p < npr) pair_step(p, c_j1[p], c_j2[p], c_x1[p], c_x2[p]);
+      if (p < npr) pair_step(p, c_jd[p], c_xd[p]);
     for (int p = NSP_CACHE; p < npr; p++) {
-      float j1, j2, x1, x2;
-      const int e = rlane_i(pr_e, p);
+      float jd, xd;
 #ifndef AW_NOSLIP_NOLDS
-      if (p < NSP_CACHE + NSP_LDS) {   // X rows parked in LDS, J rows from LDS / the spill block
+      if (p < NSP_CACHE + NSP_LDS) {   // parked in LDS
         const float* slot = xpark_slot(s, p - NSP_CACHE);
-        j1 = jval(e);
-        j2 = jval(e + 1);
-        x1 = lane < MAXV ? slot[lane] : 0.f;
-        x2 = lane < MAXV ? slot[MAXV + lane] : 0.f;
+        jd = lane < MAXV ? slot[lane] : 0.f;
+        xd = lane < MAXV ? slot[MAXV + lane] : 0.f;
       } else
 #endif
-        edge_rows(e, j1, j2, x1, x2);
-      pair_step(p, j1, j2, x1, x2);
+        pair_rows(rlane_i(pr_e, p), jd, xd);
+      pair_step(p, jd, xd);
     }
     if (impr * scale < m.noslip_tolerance) break;
   }
