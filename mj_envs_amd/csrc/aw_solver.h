@@ -1000,12 +1000,14 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
     // (r1 - r2) d1 + K d1^2 / 2 and qacc moves along xd.
     auto pair_step = [&](int p, float jd, float xd) {
       const int e = rlane_i(pr_e, p);
-      const float rd = wave_sum(jd * qacc) - rlane(pr_ard, p);
       const float f1 = fd_get(e), f2 = fd_get(e + 1);
-      const float sum = f1 + f2, x = f1 - f2;
-      const float xn = clampf(x - 2.f * rd * rlane(pr_ik, p), -sum, sum);
-      const float f1n = 0.5f * (sum + xn), f2n = 0.5f * (sum - xn);
-      const float d1 = f1n - f1;
+      const float ik = rlane(pr_ik, p), ard = rlane(pr_ard, p);
+      const float sq = wave_sum(jd * qacc);
+      // x' = clamp(x - 2 rd / K, -sum, sum) with x = f1 - f2, sum = f1 + f2 gives
+      // d1 = (x' - x) / 2 = med3(-rd / K, -f1, f2): three ops on the qacc chain after the sum
+      const float d1 = __builtin_amdgcn_fmed3f(fmaf(-sq, ik, ard * ik), -f1, f2);
+      const float rd = sq - ard;
+      const float f1n = f1 + d1, f2n = f2 - d1;
       impr -= rd * d1 + 0.5f * rlane(pr_k, p) * d1 * d1;
       qacc = fmaf(xd, d1, qacc);
       if (e < 64) {
