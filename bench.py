@@ -87,39 +87,42 @@ def cpu_baseline(blob, env_id, local, budget_s=12.0):
                        f"capacities), OpenMP over envs; threads = the job's CPU share (affinity / OMP_NUM_THREADS)")
 
 
-def same_run_parity(blob, env_id, sim, local, n=256):
-    """One env-step from the benchmark's own mid-run states (first n envs) on the GPU and on the
-    fp64 oracle: fraction within the one-step tolerance of tests/test_gpu_parity.py and errors."""
+def same_run_parity(blob, sim, n=256):
+    """One env-step of the benchmark's OWN handle (all its envs, the timed run's launch
+    configuration: persistent workgroups claiming envs past the resident slots) from its mid-run
+    states, checked on n envs sampled evenly across the whole batch against the fp64 oracle from
+    the same pre-step states: fraction within the one-step tolerance of tests/test_gpu_parity.py
+    and the errors.  Runs after the timed region (no auto-reset in this step)."""
     import numpy as np
     import torch
-    from mj_envs_amd import _native
     from oracle.pyoracle import Oracle, build
     build()
-    q, v, w, p = (sim.empty(sim.n_envs, sim.nq), sim.empty(sim.n_envs, sim.nv), sim.empty(sim.n_envs, sim.nv),
-                  sim.empty(sim.n_envs, sim.nparam))
+    N = sim.n_envs
+    q, v, w, p = sim.empty(N, sim.nq), sim.empty(N, sim.nv), sim.empty(N, sim.nv), sim.empty(N, sim.nparam)
     sim.get_state(q, v, w, p)
-    small = _native.Sim(blob, n, device=local)
-    small.set_state(q[:n].contiguous(), v[:n].contiguous(), w[:n].contiguous(), p[:n].contiguous())
-    act = small.empty(n, small.nu)
-    small.random_actions(act, 12345, 0)
-    obs, rew = small.empty(n, small.obs_dim), small.empty(n)
-    done, goal = small.empty(n, dtype=torch.uint8), small.empty(n, dtype=torch.uint8)
-    small.step(act, obs, rew, done, goal)
-    q2, v2 = small.empty(n, small.nq), small.empty(n, small.nv)
-    small.get_state(q2, v2)
+    act = sim.empty(N, sim.nu)
+    sim.random_actions(act, 12345, 0)
+    obs, rew = sim.empty(N, sim.obs_dim), sim.empty(N)
+    done, goal = sim.empty(N, dtype=torch.uint8), sim.empty(N, dtype=torch.uint8)
+    sim.step(act, obs, rew, done, goal)
+    q2, v2 = sim.empty(N, sim.nq), sim.empty(N, sim.nv)
+    sim.get_state(q2, v2)
     torch.cuda.synchronize()
-    st = dict(qpos=q[:n].cpu().numpy().astype(np.float64), qvel=v[:n].cpu().numpy().astype(np.float64),
-              warm=w[:n].cpu().numpy().astype(np.float64), params=p[:n].cpu().numpy().astype(np.float64))
+    idx = np.unique(np.linspace(0, N - 1, min(n, N)).round().astype(int))
+    g = lambda t: t.cpu().numpy()[idx].astype(np.float64)
+    st = dict(qpos=g(q), qvel=g(v), warm=g(w), params=g(p))
     o = Oracle(blob)
-    o_obs, o_rew, _, _, _ = o.step(st, act.cpu().numpy().astype(np.float64))
-    qg, vg = q2.cpu().numpy(), v2.cpu().numpy()
+    o_obs, o_rew, _, _, _ = o.step(st, g(act))
+    qg, vg = q2.cpu().numpy()[idx], v2.cpu().numpy()[idx]
     okq = (np.abs(qg - st["qpos"]) <= 2e-5 + 1e-5 * np.abs(st["qpos"])).all(axis=1)
     okv = (np.abs(vg - st["qvel"]) <= 5e-3 * (1 + np.abs(st["qvel"]))).all(axis=1)
-    small.close()
-    return dict(envs=n, frac_within_tol=round(float((okq & okv).mean()), 4),
+    ok = okq & okv
+    return dict(envs=len(idx), handle_envs=N, grid=sim.grid, sampled="evenly over the whole batch (incl. "
+                f"{int((idx >= sim.grid).sum())} envs past the {sim.grid} resident slots)",
+                frac_within_tol=round(float(ok.mean()), 4), misses=[int(i) for i in idx[~ok]],
                 max_abs_qpos=float(np.abs(qg - st["qpos"]).max()),
-                median_abs_obs=float(np.median(np.abs(obs.cpu().numpy() - o_obs))),
-                max_abs_reward=float(np.abs(rew.cpu().numpy() - o_rew).max()),
+                median_abs_obs=float(np.median(np.abs(obs.cpu().numpy()[idx] - o_obs))),
+                max_abs_reward=float(np.abs(rew.cpu().numpy()[idx] - o_rew).max()),
                 tolerance="qpos 2e-5 + 1e-5|q|, qvel 5e-3 (1 + |v|) per env (tests/test_gpu_parity.py)")
 
 
@@ -181,9 +184,6 @@ def main():
     ap.add_argument("--policy", choices=("none", "random-mlp", "dapg"), default="none",
                     help="closed loop: actions from the on-device Gaussian MLP (k_mlp): random init 32x32 "
                          "(sampled), or the reference's pretrained DAPG policy (mean action)")
-    ap.add_argument("--mpr", choices=("task", "fp32", "fp64"), default="task",
-                    help="precision of the MPR (cylinder) collider: the task's default (tasks.py "
-                         "TaskSpec.mpr_fp64; hammer fp32), or forced")
     ap.add_argument("--depth", action="store_true",
                     help="BASELINE config 5: + 64x64 depth-camera obs every env-step (default 8192 envs)")
     args = ap.parse_args()
@@ -193,7 +193,7 @@ def main():
     import torch.distributed as dist
     from mj_envs_amd import _native, perfmodel
     from mj_envs_amd.dist import EpisodeTotals, shard_from_env, stagger_phases
-    from mj_envs_amd.tasks import TASKS, attach_task, load_model
+    from mj_envs_amd.tasks import attach_task, load_model
 
     if args.depth and args.envs_per_gpu == 65536:
         args.envs_per_gpu = 8192
@@ -215,9 +215,6 @@ def main():
     blob = m.to_blob()
     n = args.envs_per_gpu
     sim = _native.Sim(blob, n, device=local, env_offset=shard.env_offset)   # streams keyed by global id
-    if args.mpr != "task":
-        sim.set_option(disableflags=_native.DSBL_MPR_FP64 if args.mpr == "fp32" else _native.DSBL_MPR_FP32)
-    mpr64 = args.mpr == "fp64" or (args.mpr == "task" and TASKS[env_id].mpr_fp64)
     obs = sim.empty(n, sim.obs_dim)
     act = sim.empty(n, sim.nu)
     rew = sim.empty(n)
@@ -331,7 +328,7 @@ def main():
             workload = workload.replace("random policy", "random policy + 64x64 depth-camera obs (HIP ray "
                                         "caster, BASELINE config 5)")
             roof["depth_kernel_ms"] = round(depth_ms, 4)
-        workload += ", MPR collider in " + ("fp64" if mpr64 else "fp32")
+        workload += ", MPR (cylinder) collider in fp64 on fp64 geometry"
         metric = "env-steps/sec at N parallel envs, hammer-v0, 1/2/4/8 MI355X"
         if env_id != "hammer-v0":   # BASELINE config 3 lines are labelled with their own task
             metric = f"env-steps/sec at N parallel envs, {env_id}, 1/2/4/8 MI355X"
@@ -353,10 +350,10 @@ def main():
                     episodes=episodes)
         if world == 1 and not args.no_parity:
             try:
-                line["parity_one_step"] = same_run_parity(blob, env_id, sim, local)
+                line["parity_one_step"] = same_run_parity(blob, sim)
             except Exception as e:
                 line["parity_one_step"] = dict(error=str(e))
-        if world == 1 and env_id == ENV_ID and depth is None and pol is None and n == 65536 and args.mpr == "task" \
+        if world == 1 and env_id == ENV_ID and depth is None and pol is None and n == 65536 \
                 and not args.no_config2:
             line["config2_4096_envs"] = config2(blob, env_id, local)
         if world == 1 and not args.no_cpu_baseline:

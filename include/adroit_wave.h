@@ -55,11 +55,13 @@ enum {
 
 /* aw_dims() output order.  MAXCON / MAXEFC / MAXDENSE: the kernel's per-env capacities for
  * contacts, constraint rows and dense (contact) rows; the reference's are nconmax 100 /
- * njmax 500 (DAPG_assets.xml:4).  A step that needs more raises AW_ST_*_OVERFLOW. */
+ * njmax 500 (DAPG_assets.xml:4).  A step that needs more raises AW_ST_*_OVERFLOW.
+ * GRID: workgroups of one aw_step launch (one per resident slot on the device, capped at
+ * n_envs); below n_envs the persistent workgroups claim the remaining envs from a counter. */
 enum {
   AW_DIM_NQ, AW_DIM_NV, AW_DIM_NU, AW_DIM_OBS, AW_DIM_NPARAM, AW_DIM_FRAME_SKIP,
   AW_DIM_HORIZON, AW_DIM_TASK, AW_DIM_NENV, AW_DIM_NBODY, AW_DIM_NSITE, AW_DIM_NGEOM,
-  AW_DIM_NPAIR, AW_DIM_MAXCON, AW_DIM_MAXEFC, AW_DIM_MAXDENSE, AW_NDIMS
+  AW_DIM_NPAIR, AW_DIM_MAXCON, AW_DIM_MAXEFC, AW_DIM_MAXDENSE, AW_DIM_GRID, AW_NDIMS
 };
 
 /* model table = Model.to_blob() of mj_envs_amd/mjcf.py with the task block attached
@@ -68,11 +70,11 @@ int aw_create(const void* blob, size_t nbytes, int n_envs, int device, aw_handle
 int aw_destroy(aw_handle* h);
 int aw_dims(const aw_handle* h, int* dims /* [AW_NDIMS] */);
 
-/* MuJoCo-style disable flags (mjtDisableBit values; bit 14 = noslip, bit 15 = explicit
- * damping, bit 16 = MPR (cylinder) collider in fp32, bit 17 = MPR collider in fp64; neither:
- * the task's default from the model blob, task_mpr_fp64) and solver iteration counts;
- * negative values keep the current setting.  Waits for the device (queued steps finish with
- * the old options), then re-uploads the model header that k_step reads. */
+/* MuJoCo-style disable flags (mjtDisableBit values, bits 0..15; bit 14 = noslip, bit 15 =
+ * explicit damping; higher bits: AW_EUNSUPPORTED -- the MPR (cylinder) collider always runs in
+ * fp64 on fp64 geometry) and solver iteration counts; negative values keep the current setting.
+ * Waits for the device (queued steps finish with the old options), then re-uploads the model
+ * header that k_step reads. */
 int aw_set_option(aw_handle* h, int disableflags, int iterations, int noslip_iterations);
 
 /* Reset envs (mask[e] != 0, or all if mask == NULL): qpos = qpos0, qvel = 0, warmstart = 0,
@@ -121,6 +123,15 @@ int aw_episode_stats(aw_handle* h, float* last_return, int32_t* last_goal_steps,
  * successful episodes (> task success_steps goal steps: hammer_v0.py:167-175, pen_v0.py:180-188) */
 int aw_episode_totals(aw_handle* h, int32_t* episodes, float* sum_return, int32_t* successes,
                       void* stream);
+
+/* Restore the running totals (checkpoint / resume): finished-episode count, summed return,
+ * successes.  The finished-episode count is also the Philox episode key of the reset draws, so a
+ * checkpoint restores it once, here or through aw_set_episode, with the same value.  A complete
+ * checkpoint is aw_get_state (qpos, qvel, warmstart, params) + aw_get_episode (ep_len, ep_ret,
+ * ep_goal) + aw_episode_totals (episodes, sum_return, successes), restored with aw_set_state,
+ * aw_set_episode and aw_set_episode_totals. */
+int aw_set_episode_totals(aw_handle* h, const int32_t* episodes, const float* sum_return,
+                          const int32_t* successes, void* stream);
 
 /* episode bookkeeping of the running episode (checkpoint / resume, staggered starts): steps
  * taken, return so far, goal steps so far, finished-episode count; any pointer may be NULL */

@@ -17,10 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # AW_LIB selects a diagnostic build (e.g. libadroit_hip_prof.so with the stage profiler)
 LIB_PATH = os.environ.get("AW_LIB") or os.path.join(HERE, "libadroit_hip.so")
 
-AW_NDIMS = 16
-# aw_set_option bits of ours: MPR (cylinder) collider in fp32 / in fp64 (neither: the task default)
-DSBL_MPR_FP64 = 1 << 16
-DSBL_MPR_FP32 = 1 << 17
+AW_NDIMS = 17
 # kernel capacities (aw_common.h; also reported by aw_dims)
 MAXCON, MAXEFC, MAXDENSE = 48, 192, 128
 ST_BADQPOS, ST_BADQVEL, ST_BADQACC, ST_CON_OVERFLOW, ST_EFC_OVERFLOW = 1, 2, 4, 8, 16
@@ -70,6 +67,7 @@ def load():
     L.aw_episode_totals.argtypes = [_vp, _vp, _vp, _vp, _vp]
     L.aw_get_episode.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp]
     L.aw_set_episode.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp]
+    L.aw_set_episode_totals.argtypes = [_vp, _vp, _vp, _vp, _vp]
     L.aw_get_state.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp]
     L.aw_set_state.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp]
     L.aw_status.argtypes = [_vp, _vp, _vp, _vp]
@@ -91,7 +89,7 @@ def load():
     for f in ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "aw_step",
               "aw_random_actions", "aw_get_state", "aw_set_state", "aw_status", "aw_episode_stats",
               "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_set_env_offset", "aw_clear_status",
-              "aw_episode_totals", "aw_get_episode", "aw_set_episode"):
+              "aw_episode_totals", "aw_get_episode", "aw_set_episode", "aw_set_episode_totals"):
         getattr(L, f).restype = ctypes.c_int
     _lib = L
     return L
@@ -99,7 +97,8 @@ def load():
 
 EXPORTS = ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "aw_step",
            "aw_random_actions", "aw_set_env_offset", "aw_get_state", "aw_set_state", "aw_status",
-           "aw_clear_status", "aw_episode_stats", "aw_episode_totals", "aw_get_episode", "aw_set_episode",
+           "aw_clear_status", "aw_episode_stats", "aw_episode_totals", "aw_set_episode_totals", "aw_get_episode",
+           "aw_set_episode",
            "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_render_depth", "aw_policy_mlp",
            "aw_collide_test", "aw_last_error")
 
@@ -121,6 +120,7 @@ def stage_profile(reset: bool = True) -> dict:
     for i, name in enumerate(SUBSTAGES):
         out[name] = v[19 + i]
     out["offd_rows"] = v[38]
+    out["co_kin64"] = v[39]
     return out
 
 
@@ -157,7 +157,7 @@ class Sim:
         _check(L.aw_dims(self.h, d))
         (self.nq, self.nv, self.nu, self.obs_dim, self.nparam, self.frame_skip, self.horizon,
          self.task_kind, self.n_envs, self.nbody, self.nsite, self.ngeom, self.npair,
-         self.maxcon, self.maxefc, self.maxdense) = list(d)
+         self.maxcon, self.maxefc, self.maxdense, self.grid) = list(d)
         self.env_offset = 0
         if env_offset:
             self.set_env_offset(env_offset)
@@ -213,6 +213,10 @@ class Sim:
 
     def episode_totals(self, episodes=None, sum_return=None, successes=None):
         _check(load().aw_episode_totals(self.h, _ptr(episodes), _ptr(sum_return), _ptr(successes), _stream()))
+
+    def set_episode_totals(self, episodes=None, sum_return=None, successes=None):
+        """restore the running totals (checkpoint); see include/adroit_wave.h aw_set_episode_totals"""
+        _check(load().aw_set_episode_totals(self.h, _ptr(episodes), _ptr(sum_return), _ptr(successes), _stream()))
 
     def get_episode(self, ep_len=None, ep_ret=None, ep_goal=None, episodes=None):
         _check(load().aw_get_episode(self.h, _ptr(ep_len), _ptr(ep_ret), _ptr(ep_goal), _ptr(episodes),

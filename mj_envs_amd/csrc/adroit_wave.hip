@@ -76,18 +76,17 @@ AW_DEV void sort_contacts(Env& s, int lane) {
 }
 
 // narrowphase over the broadphase survivors of one collider class
-template <int C, int MP>
+template <int C>
 AW_DEV void narrow_class(const DModel& m, Env& s, const short* plist, int cnt, int lane) {
   const int st = m.cls_start[C];
-  for (int i = lane; i < cnt; i += 64) collide_pair<C, MP>(m, s, plist[st + i]);
+  for (int i = lane; i < cnt; i += 64) collide_pair<C>(m, s, plist[st + i]);
 }
 
 // mj_collision: bounding-sphere broadphase over the static candidate list (one pair per lane,
 // 64 per round), survivors compacted class-major into an LDS list (ballot + mbcnt), then ONE
 // narrowphase loop over the list: lanes of a round mostly share a collider, instead of every
-// round executing every collider branch its lanes happen to need.
-// MP: precision of the MPR collider (MPR_FP32 / MPR_FP64), a kernel template parameter
-template <int MP>
+// round executing every collider branch its lanes happen to need.  MPR pairs (class 4) run on
+// fp64 geometry: stage_kin64 computes their bodies' frames once the broadphase has kept one.
 AW_DEV void stage_collision(const DModel& m, Env& s, int lane) {
   if (lane == 0) s.ncon = 0;
   wsync();
@@ -124,15 +123,19 @@ AW_DEV void stage_collision(const DModel& m, Env& s, int lane) {
     }
     AW_PROF(s, PR_CO_BROAD);
     wsync();
-    narrow_class<0, MP>(m, s, plist, cnt[0], lane);
+    narrow_class<0>(m, s, plist, cnt[0], lane);
     AW_PROF(s, PR_CO_C0);
-    narrow_class<1, MP>(m, s, plist, cnt[1], lane);
+    narrow_class<1>(m, s, plist, cnt[1], lane);
     AW_PROF(s, PR_CO_C1);
-    narrow_class<2, MP>(m, s, plist, cnt[2], lane);
+    narrow_class<2>(m, s, plist, cnt[2], lane);
     AW_PROF(s, PR_CO_C2);
-    narrow_class<3, MP>(m, s, plist, cnt[3], lane);
+    narrow_class<3>(m, s, plist, cnt[3], lane);
     AW_PROF(s, PR_CO_C3);
-    narrow_class<4, MP>(m, s, plist, cnt[4], lane);
+    if (cnt[4] > 0) {
+      stage_kin64(m, s, lane);
+      AW_PROF(s, PR_CO_KIN64);
+      narrow_class<4>(m, s, plist, cnt[4], lane);
+    }
   }
   wsync();
   AW_PROF(s, PR_CO_NARROW);
@@ -147,11 +150,11 @@ struct Dof {
 // mj_forward: everything up to qacc / forces / sensors; Mrow is left in registers.  Stage order
 // follows the LDS overlays (aw_common.h Env): the constraint rows are assembled while the
 // phase-K arrays (cdof, subcom) are alive, then the solver phase reuses that storage.
-template <int NV, int MP>
+template <int NV, bool KEEP_D = false>
 AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV], Dof& d) {
   stage_kinematics(m, s, lane);
   AW_PROF(s, PR_KIN);
-  stage_collision<MP>(m, s, lane);
+  stage_collision(m, s, lane);
   AW_PROF(s, PR_COLL);
   stage_com(m, s, lane);
   AW_PROF(s, PR_COM);
@@ -184,7 +187,7 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV], Dof& d
     float a = 0.f;
     solve_newton<NV>(m, s, lane, Mrow, a, d.qfrc_smooth, d.qacc_smooth);
     AW_PROF(s, PR_NEWTON);
-    if (m.noslip_iterations > 0 && !(m.disableflags & DSBL_NOSLIP)) solve_noslip<NV>(m, s, lane, Mrow, a);
+    if (m.noslip_iterations > 0 && !(m.disableflags & DSBL_NOSLIP)) solve_noslip<NV, KEEP_D>(m, s, lane, Mrow, a);
     AW_PROF(s, PR_NOSLIP);
     for (int r = lane; r < s.nefc; r += 64) s.rowbuf[r] = s.efc_force[r];
     wsync();
@@ -312,13 +315,13 @@ AW_DEV void reset_prepare(const DModel& m, Env& s, const DState& st, int env, in
 }
 
 // reset one env in LDS: params (given or sampled), qpos0/0/0, forward, obs
-template <int NV, int MP>
+template <int NV>
 AW_DEV void reset_env(const DModel& m, Env& s, const DState& st, int env, int lane,
                       const float* params_in, uint64_t seed, float* obs) {
   reset_prepare<NV>(m, s, st, env, lane, params_in, seed);
   float Mrow[NV];
   Dof d;
-  forward<NV, MP>(m, s, lane, Mrow, d);
+  forward<NV>(m, s, lane, Mrow, d);
   if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
 }
 
@@ -326,7 +329,7 @@ AW_DEV void reset_env(const DModel& m, Env& s, const DState& st, int env, int la
 // in-kernel auto-reset.  forward<NV> has exactly ONE inlined call site (the loop below drives
 // substeps, the mj_checkAcc retry and the reset forward through it), which keeps the code
 // object small enough for the instruction cache.
-template <int NV, int MP>
+template <int NV>
 __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DModel* __restrict__ mptr, DState stval,
                                              int n, const float* __restrict__ actions,
                                              float* obs, float* reward, uint8_t* done, uint8_t* goal,
@@ -375,7 +378,7 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
       asm volatile("" ::: "memory");
       if (!resetting && !retry) check_state<NV>(s, lane);
       AW_PROF(s, PR_CHECK);
-      forward<NV, MP>(m, s, lane, Mrow, d);
+      forward<NV>(m, s, lane, Mrow, d);
       if (resetting) break;
       if (!retry && check_acc<NV>(s, lane, d)) { retry = true; continue; }
       retry = false;
@@ -442,7 +445,7 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
   }
 }
 
-template <int NV, int MP>
+template <int NV>
 __global__ void __launch_bounds__(64) k_reset(DModel m, DState st, int n, const uint8_t* mask,
                                               const float* params, uint64_t seed, float* obs) {
   __shared__ Env s;
@@ -450,12 +453,12 @@ __global__ void __launch_bounds__(64) k_reset(DModel m, DState st, int n, const 
   if (env >= n) return;
   if (mask && !mask[env]) return;
   if (lane == 0) { s.status = 0u; s.slot = blockIdx.x; }
-  reset_env<NV, MP>(m, s, st, env, lane, params, seed, obs);
+  reset_env<NV>(m, s, st, env, lane, params, seed, obs);
   store_env<NV>(m, s, st, env, lane);
   if (lane == 0) { st.status[env] = s.status; st.status_acc[env] |= s.status; }
 }
 
-template <int NV, int MP>
+template <int NV>
 __global__ void __launch_bounds__(64) k_set_state(DModel m, DState st, int n, const float* qpos,
                                                   const float* qvel, const float* warm,
                                                   const float* params, float* obs) {
@@ -475,7 +478,7 @@ __global__ void __launch_bounds__(64) k_set_state(DModel m, DState st, int n, co
   stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
   float Mrow[NV];
   Dof d;
-  forward<NV, MP>(m, s, lane, Mrow, d);
+  forward<NV>(m, s, lane, Mrow, d);
   if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
   store_env<NV>(m, s, st, env, lane);
   if (lane == 0) { st.status[env] = s.status; st.status_acc[env] |= s.status; }
@@ -484,7 +487,7 @@ __global__ void __launch_bounds__(64) k_set_state(DModel m, DState st, int n, co
 // dump layout (floats): see mj_envs_amd/_native.py dump_layout (same offsets from the capacities)
 constexpr int DUMP_SCAL = 1760, DUMP_CON = 1768, DUMP_EFC = DUMP_CON + 14 * MAXCON;
 static_assert(DUMP_EFC + 4 * MAXEFC == AW_DUMP_SIZE, "AW_DUMP_SIZE out of date");
-template <int NV, int MP>
+template <int NV>
 __global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const float* ctrl, float* out) {
   __shared__ Env s;
   const int lane = threadIdx.x;
@@ -493,7 +496,7 @@ __global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const
   stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
   float Mrow[NV];
   Dof d;
-  forward<NV, MP>(m, s, lane, Mrow, d);
+  forward<NV, true>(m, s, lane, Mrow, d);   // efc_D kept out of noslip's parking
   for (int i = lane; i < MAXB * 3; i += 64) out[i] = i < m.nbody * 3 ? (&s.xpos[0][0])[i] : 0.f;
   for (int i = lane; i < MAXB * 4; i += 64) out[96 + i] = i < m.nbody * 4 ? (&s.xquat[0][0])[i] : 0.f;
   for (int i = lane; i < MAXS * 3; i += 64) out[224 + i] = i < m.nsite * 3 ? (&s.sxpos[0][0])[i] : 0.f;
@@ -555,7 +558,6 @@ __global__ void __launch_bounds__(64) k_task_eval(DModel m, int n, const float* 
 
 // Test hook (aw_collide_test): the narrowphase of one primitive pair per workgroup, given world
 // poses -- exact-geometry collider tests against the oracle's colliders.
-template <int MP>
 AW_DEV void collide_gv(const DModel& m, const GV& a, const GV& b, float margin, Emit& e) {
   const int lo = a.type, hi = b.type;   // a.type <= b.type
   if (lo == GEOM_PLANE) {
@@ -564,8 +566,11 @@ AW_DEV void collide_gv(const DModel& m, const GV& a, const GV& b, float margin, 
     else if (hi == GEOM_CYLINDER) c_plane_cylinder(a, b, margin, e);
     else if (hi == GEOM_BOX) c_plane_box(a, b, margin, e);
   } else if (lo == GEOM_CYLINDER || hi == GEOM_CYLINDER) {
-    if (MP) c_convex<double>(m, a, b, margin, e);
-    else c_convex<float>(m, a, b, margin, e);
+    mpr::GVdT<double> ad, bd;
+    for (int k = 0; k < 3; k++) { ad.pos[k] = a.pos[k]; ad.size[k] = a.size[k]; bd.pos[k] = b.pos[k]; bd.size[k] = b.size[k]; }
+    for (int k = 0; k < 9; k++) { ad.mat[k] = a.mat[k]; bd.mat[k] = b.mat[k]; }
+    ad.type = a.type; bd.type = b.type;
+    c_convex64(m, ad, bd, (double)margin, e);
   } else if (hi == GEOM_BOX && lo == GEOM_BOX) {
     c_box_box(a, b, margin, e);
   } else if (hi == GEOM_BOX) {
@@ -580,7 +585,6 @@ AW_DEV void collide_gv(const DModel& m, const GV& a, const GV& b, float margin, 
   }
 }
 
-template <int MP>
 __global__ void __launch_bounds__(64) k_collide_test(DModel m, int n, const int* types, const float* pos,
                                                      const float* mat, const float* size, const float* margin,
                                                      float* out, int* count) {
@@ -598,7 +602,7 @@ __global__ void __launch_bounds__(64) k_collide_test(DModel m, int n, const int*
     }
     const int f = g[0].type <= g[1].type ? 0 : 1;
     Emit e{&s, 0, 0};
-    collide_gv<MP>(m, g[f], g[1 - f], margin[i], e);
+    collide_gv(m, g[f], g[1 - f], margin[i], e);
   }
   wsync();
   const int nc = s.ncon < MAXPAIRCON ? s.ncon : MAXPAIRCON;
@@ -692,13 +696,15 @@ std::vector<float> tof(const std::vector<double>& v) { return std::vector<float>
 
 struct aw_handle {
   int device, nenv, NV;
-  int mpr_fp64;   // the task's MPR collider precision (blob task_mpr_fp64); see mpr_kernel_fp64()
   DModel m;
   DState st;
   void* dmodel = nullptr;
   void* dmhdr = nullptr;   // device copy of m (k_step reads its scalars from here)
   void* dstate = nullptr;
   int* next_env = nullptr;   // k_step's work counter (env claims past the first grid's worth)
+  int slots = 0;             // persistent k_step grid: resident workgroups of the selected instantiation,
+                             // or AW_STEP_GRID (read at aw_create; 0 = one workgroup per env)
+  int grid_env = -1;         // AW_STEP_GRID at create (-1: unset)
 };
 
 static int upload_header(aw_handle* h) {
@@ -726,6 +732,7 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
   m.noslip_tolerance = (float)B.opt("noslip_tolerance", 1e-6);
   m.mpr_tolerance = (float)B.opt("mpr_tolerance", 1e-6);
   m.mpr_iterations = (int)B.opt("mpr_iterations", 50);
+  m.mpr_tolerance64 = B.opt("mpr_tolerance", 1e-6);
   m.meaninertia = (float)B.opt("meaninertia", 1);
   m.pen_length = (float)B.opt("task_pen_length", 1);
   m.tar_length = (float)B.opt("task_tar_length", 1);
@@ -775,6 +782,8 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
   PUT(body_invweight0, tof(B.f("body_invweight0")));
   PUT(body_subtreemass, tof(B.f("body_subtreemass")));
   PUT(body_dofmask, bmask);
+  PUT(body_pos64, B.f("body_pos")); PUT(body_quat64, B.f("body_quat"));
+  PUT(jnt_pos64, B.f("jnt_pos")); PUT(jnt_axis64, B.f("jnt_axis"));
 
   std::vector<int> jtype = B.i("jnt_type");
   for (int t : jtype) if (t != JNT_HINGE && t != JNT_SLIDE) return fail(AW_EUNSUPPORTED, "joint type");
@@ -809,14 +818,18 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
                       grb = B.f("geom_rbound");
   std::vector<int> gmap(ngeom_all, -1), ctype, cbody;
   std::vector<float> cpos, cquat, csize, crb;
+  std::vector<double> cpos64, cquat64, csize64;
   for (int g = 0; g < ngeom_all; g++) {
     if (gtype[g] == 7 || (gcon[g] == 0 && gaff[g] == 0)) continue;
     gmap[g] = (int)ctype.size();
     ctype.push_back(gtype[g]); cbody.push_back(gbody[g]);
     for (int k = 0; k < 3; k++) { cpos.push_back((float)gpos[3 * g + k]); csize.push_back((float)gsize[3 * g + k]); }
     for (int k = 0; k < 4; k++) cquat.push_back((float)gquat[4 * g + k]);
+    for (int k = 0; k < 3; k++) { cpos64.push_back(gpos[3 * g + k]); csize64.push_back(gsize[3 * g + k]); }
+    for (int k = 0; k < 4; k++) cquat64.push_back(gquat[4 * g + k]);
     crb.push_back((float)grb[g]);
   }
+  PUT(geom_pos64, cpos64); PUT(geom_quat64, cquat64); PUT(geom_size64, csize64);
   m.ngeom = (int)ctype.size();
   if (m.ngeom > MAXG) return fail(AW_EUNSUPPORTED, "too many collidable geoms");
   PUT(geom_type, ctype); PUT(geom_bodyid, cbody); PUT(geom_pos, cpos);
@@ -859,6 +872,7 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
   // mj_contactParam with equal priorities)
   std::vector<int> pg1, pg2, pcd;
   std::vector<float> pfr, psr, psi, pmg, pgp;
+  std::vector<double> pmg64;
   {
     std::vector<int> e1 = B.i("pair_geom1"), e2 = B.i("pair_geom2"), ecd = B.i("pair_condim");
     std::vector<double> efr = B.f("pair_friction"), esr = B.f("pair_solref"), esi = B.f("pair_solimp"),
@@ -869,7 +883,7 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
       for (int k = 0; k < 5; k++) pfr.push_back((float)efr[5 * p + k]);
       for (int k = 0; k < 2; k++) psr.push_back((float)esr[2 * p + k]);
       for (int k = 0; k < 5; k++) psi.push_back((float)esi[5 * p + k]);
-      pmg.push_back((float)emg[p]); pgp.push_back((float)egp[p]);
+      pmg.push_back((float)emg[p]); pgp.push_back((float)egp[p]); pmg64.push_back(emg[p]);
     }
     std::vector<int> c1v = B.i("cand_geom1"), c2v = B.i("cand_geom2"), gcd = B.i("geom_condim");
     std::vector<double> gfr = B.f("geom_friction"), gsm = B.f("geom_solmix"), gsr = B.f("geom_solref"),
@@ -889,6 +903,7 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
       for (int k = 0; k < 2; k++) psr.push_back((float)(mix * gsr[2 * a + k] + (1 - mix) * gsr[2 * b + k]));
       for (int k = 0; k < 5; k++) psi.push_back((float)(mix * gsi[5 * a + k] + (1 - mix) * gsi[5 * b + k]));
       pmg.push_back((float)std::max(gmg[a], gmg[b])); pgp.push_back((float)std::max(ggp[a], ggp[b]));
+      pmg64.push_back(std::max(gmg[a], gmg[b]));
     }
   }
   m.npairall = (int)pg1.size();
@@ -914,7 +929,14 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
     m.cls_start[0] = 0;
     for (int c = 0; c < NCLASS; c++) m.cls_start[c + 1] = m.cls_start[c] + ccount[c];
     if (m.npairall > JL * VS * 2) return fail(AW_EUNSUPPORTED, "too many collision pairs");
-    PUT(cp_class, pcls); PUT(cp_rb, prb);
+    PUT(cp_class, pcls); PUT(cp_rb, prb); PUT(cp_margin64, pmg64);
+    // bodies whose fp64 frames the MPR pairs read (stage_kin64): the pairs' bodies + ancestors
+    std::vector<int> k64(nbody, 0);
+    for (int p = 0; p < m.npairall; p++)
+      if (pcls[p] == 4)
+        for (int g : {pg1[p], pg2[p]})
+          for (int b = cbody[g]; b > 0; b = parent[b]) k64[b] = 1;
+    PUT(body_kin64, k64);
     std::vector<int> ppack(m.npairall);
     for (int p = 0; p < m.npairall; p++) ppack[p] = pcls[p] | (pg1[p] << 8) | (pg2[p] << 16);
     PUT(cp_pack, ppack);
@@ -996,50 +1018,41 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
   return AW_OK;
 }
 
-template <int NV, int MP>
+// resident k_step workgroups on the handle's device (occupancy x CUs): the persistent grid
+template <int NV>
+static int step_slots(int device) {
+  int per_cu = 0, cus = 0;
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_step<NV>, 64, 0);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  return std::max(per_cu, 1) * std::max(cus, 1);
+}
+template <int NV>
 static void launch_step(aw_handle* h, const float* a, float* obs, float* rew, uint8_t* done, uint8_t* goal,
                         float* tobs, int autoreset, uint64_t seed, hipStream_t st) {
-  // grid = the workgroups the chip holds at once (occupancy x CUs), capped at nenv;
-  // AW_STEP_GRID=<n> overrides (0: one workgroup per env, the non-persistent launch)
-  static int slots = -1;
-  if (slots < 0) {
-    int per_cu = 0, cus = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_step<NV, MP>, 64, 0);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
-    slots = std::max(per_cu, 1) * std::max(cus, 1);
-    if (const char* e = getenv("AW_STEP_GRID")) slots = atoi(e) > 0 ? atoi(e) : 1 << 30;
-  }
-  const int grid = std::min(h->nenv, slots);
+  // grid = the handle's persistent slot count (aw_create / aw_set_option), capped at nenv
+  const int grid = std::min(h->nenv, h->slots);
   if (grid < h->nenv) (void)hipMemsetAsync(h->next_env, 0, sizeof(int), st);
-  hipLaunchKernelGGL((k_step<NV, MP>), dim3(grid), dim3(64), 0, st, h->m, (const DModel*)h->dmhdr, h->st, h->nenv, a, obs, rew, done,
+  hipLaunchKernelGGL((k_step<NV>), dim3(grid), dim3(64), 0, st, h->m, (const DModel*)h->dmhdr, h->st, h->nenv, a, obs, rew, done,
                      goal, tobs, autoreset, seed, h->next_env);
 }
-template <int NV, int MP>
+template <int NV>
 static void launch_reset(aw_handle* h, const uint8_t* mask, const float* params, uint64_t seed, float* obs,
                          hipStream_t st) {
-  hipLaunchKernelGGL((k_reset<NV, MP>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, mask, params, seed, obs);
+  hipLaunchKernelGGL((k_reset<NV>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, mask, params, seed, obs);
 }
-template <int NV, int MP>
+template <int NV>
 static void launch_set(aw_handle* h, const float* q, const float* v, const float* w, const float* p, float* obs,
                        hipStream_t st) {
-  hipLaunchKernelGGL((k_set_state<NV, MP>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, q, v, w, p, obs);
+  hipLaunchKernelGGL((k_set_state<NV>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, q, v, w, p, obs);
 }
-template <int NV, int MP>
+template <int NV>
 static void launch_dump(aw_handle* h, int env, const float* ctrl, float* out, hipStream_t st) {
-  hipLaunchKernelGGL((k_dump<NV, MP>), dim3(1), dim3(64), 0, st, h->m, h->st, env, ctrl, out);
+  hipLaunchKernelGGL((k_dump<NV>), dim3(1), dim3(64), 0, st, h->m, h->st, env, ctrl, out);
 }
 
 template <int NV>
 static void launch_depth(aw_handle* h, const CamRec& cam, int W, int H, float* out, hipStream_t st) {
   hipLaunchKernelGGL((k_depth<NV>), dim3(h->nenv), dim3(256), 0, st, h->m, h->st, h->nenv, cam, W, H, out);
-}
-
-// MPR precision of the forward kernels (template parameter MP): the task default unless a
-// disable bit forces one (include/adroit_wave.h aw_set_option)
-static bool mpr_kernel_fp64(const aw_handle* h) {
-  if (h->m.disableflags & DSBL_MPR_FP64) return false;
-  if (h->m.disableflags & DSBL_MPR_FP32) return true;
-  return h->mpr_fp64 != 0;
 }
 
 #ifdef AW_ONLY_NV
@@ -1057,6 +1070,18 @@ static bool mpr_kernel_fp64(const aw_handle* h) {
     default: return fail(AW_EUNSUPPORTED, "nv not instantiated (30/33/36)");      \
   }
 #endif
+
+// persistent grid of the k_step instantiation the handle currently selects
+static int update_slots(aw_handle* h) {
+  if (h->grid_env >= 0) {
+    h->slots = h->grid_env > 0 ? h->grid_env : (1 << 30);
+    return AW_OK;
+  }
+#define CALL(NVV) (h->slots = step_slots<NVV>(h->device))
+  DISPATCH_NV(h->NV, CALL)
+#undef CALL
+  return AW_OK;
+}
 
 extern "C" {
 
@@ -1097,7 +1122,6 @@ int aw_create(const void* blob, size_t nbytes, int n_envs, int device, aw_handle
   std::unique_ptr<MData> md(new MData());   // value-initialised: zero
   if (int rc = build_model(B, h->m, *md)) return rc;
   h->NV = h->m.nv;
-  h->mpr_fp64 = B.dim("task_mpr_fp64", 1);   // no task block: MuJoCo's fp64
   if (h->NV != 30 && h->NV != 33 && h->NV != 36) return fail(AW_EUNSUPPORTED, "nv not instantiated");
   HIPCHK(hipSetDevice(device));
   HIPCHK(hipMalloc(&h->dmodel, sizeof(MData)));
@@ -1119,6 +1143,8 @@ int aw_create(const void* blob, size_t nbytes, int n_envs, int device, aw_handle
     for (int k = 0; k < h->m.nparam; k++) prm[e * np + k] = (float)def[k];
   HIPCHK(hipMemcpy(h->st.params, prm.data(), prm.size() * 4, hipMemcpyHostToDevice));
   if (int rc2 = upload_header(h.get())) return rc2;
+  if (const char* e = getenv("AW_STEP_GRID")) h->grid_env = std::max(atoi(e), 0);
+  if (int rc3 = update_slots(h.get())) return rc3;
   *out = h.release();
   return AW_OK;
 }
@@ -1134,13 +1160,15 @@ int aw_dims(const aw_handle* h, int* d) {
   if (!h || !d) return fail(AW_EINVAL, "aw_dims: null");
   const DModel& m = h->m;
   int v[AW_NDIMS] = {m.nq, m.nv, m.nu, m.obs_dim, m.nparam, m.frame_skip, m.horizon, m.task_kind, h->nenv,
-                     m.nbody, m.nsite, m.ngeom, m.npairall, MAXCON, MAXEFC, MAXDENSE};
+                     m.nbody, m.nsite, m.ngeom, m.npairall, MAXCON, MAXEFC, MAXDENSE, std::min(h->slots, h->nenv)};
   memcpy(d, v, sizeof(v));
   return AW_OK;
 }
 
 int aw_set_option(aw_handle* h, int disableflags, int iterations, int noslip_iterations) {
   if (!h) return fail(AW_EINVAL, "aw_set_option: null");
+  if (disableflags >= 0 && (disableflags & ~0xFFFF))
+    return fail(AW_EUNSUPPORTED, "aw_set_option: only MuJoCo's disable bits 0..15 (the MPR collider always runs in fp64)");
   if (disableflags >= 0) h->m.disableflags = disableflags;
   if (iterations >= 0) h->m.iterations = iterations;
   if (noslip_iterations >= 0) h->m.noslip_iterations = noslip_iterations;
@@ -1152,7 +1180,7 @@ int aw_set_option(aw_handle* h, int disableflags, int iterations, int noslip_ite
 int aw_reset(aw_handle* h, const uint8_t* mask, const float* params, uint64_t seed, float* obs, void* stream) {
   if (!h) return fail(AW_EINVAL, "aw_reset: null");
   HIPCHK(hipSetDevice(h->device));
-#define CALL(NVV) (mpr_kernel_fp64(h) ? launch_reset<NVV, 1>(h, mask, params, seed, obs, (hipStream_t)stream) : launch_reset<NVV, 0>(h, mask, params, seed, obs, (hipStream_t)stream))
+#define CALL(NVV) launch_reset<NVV>(h, mask, params, seed, obs, (hipStream_t)stream)
   DISPATCH_NV(h->NV, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());
@@ -1163,7 +1191,7 @@ int aw_step(aw_handle* h, const float* actions, float* obs, float* reward, uint8
             float* terminal_obs, int autoreset, uint64_t seed, void* stream) {
   if (!h || !actions || !obs || !reward || !done || !goal) return fail(AW_EINVAL, "aw_step: null buffer");
   HIPCHK(hipSetDevice(h->device));
-#define CALL(NVV) (mpr_kernel_fp64(h) ? launch_step<NVV, 1>(h, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, (hipStream_t)stream) : launch_step<NVV, 0>(h, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, (hipStream_t)stream))
+#define CALL(NVV) launch_step<NVV>(h, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, (hipStream_t)stream)
   DISPATCH_NV(h->NV, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());
@@ -1197,7 +1225,7 @@ int aw_set_state(aw_handle* h, const float* qpos, const float* qvel, const float
                  float* obs, void* stream) {
   if (!h) return fail(AW_EINVAL, "aw_set_state: null");
   HIPCHK(hipSetDevice(h->device));
-#define CALL(NVV) (mpr_kernel_fp64(h) ? launch_set<NVV, 1>(h, qpos, qvel, warm, params, obs, (hipStream_t)stream) : launch_set<NVV, 0>(h, qpos, qvel, warm, params, obs, (hipStream_t)stream))
+#define CALL(NVV) launch_set<NVV>(h, qpos, qvel, warm, params, obs, (hipStream_t)stream)
   DISPATCH_NV(h->NV, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());
@@ -1265,6 +1293,18 @@ int aw_episode_totals(aw_handle* h, int32_t* episodes, float* sum_return, int32_
   return AW_OK;
 }
 
+int aw_set_episode_totals(aw_handle* h, const int32_t* episodes, const float* sum_return, const int32_t* successes,
+                          void* stream) {
+  if (!h) return fail(AW_EINVAL, "aw_set_episode_totals: null");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t b = (size_t)h->nenv * 4;
+  if (episodes) HIPCHK(hipMemcpyAsync(h->st.episode, episodes, b, hipMemcpyDeviceToDevice, st));
+  if (sum_return) HIPCHK(hipMemcpyAsync(h->st.sum_ret, sum_return, b, hipMemcpyDeviceToDevice, st));
+  if (successes) HIPCHK(hipMemcpyAsync(h->st.n_success, successes, b, hipMemcpyDeviceToDevice, st));
+  return AW_OK;
+}
+
 int aw_episode_stats(aw_handle* h, float* last_return, int32_t* last_goal, int32_t* last_len, int32_t* episodes,
                      void* stream) {
   if (!h) return fail(AW_EINVAL, "aw_episode_stats: null");
@@ -1292,7 +1332,7 @@ int aw_task_eval(aw_handle* h, int n, const float* qpos, const float* qvel, cons
 int aw_forward_dump(aw_handle* h, int env, const float* ctrl, float* out, void* stream) {
   if (!h || !out || env < 0 || env >= h->nenv) return fail(AW_EINVAL, "aw_forward_dump: bad arguments");
   HIPCHK(hipSetDevice(h->device));
-#define CALL(NVV) (mpr_kernel_fp64(h) ? launch_dump<NVV, 1>(h, env, ctrl, out, (hipStream_t)stream) : launch_dump<NVV, 0>(h, env, ctrl, out, (hipStream_t)stream))
+#define CALL(NVV) launch_dump<NVV>(h, env, ctrl, out, (hipStream_t)stream)
   DISPATCH_NV(h->NV, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());
@@ -1333,10 +1373,7 @@ int aw_collide_test(aw_handle* h, int n, const int32_t* types, const float* pos,
     return fail(AW_EINVAL, "aw_collide_test: bad arguments");
   HIPCHK(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
-  if (mpr_kernel_fp64(h))
-    hipLaunchKernelGGL(k_collide_test<1>, dim3(n), dim3(64), 0, st, h->m, n, types, pos, mat, size, margin, out, count);
-  else
-    hipLaunchKernelGGL(k_collide_test<0>, dim3(n), dim3(64), 0, st, h->m, n, types, pos, mat, size, margin, out, count);
+  hipLaunchKernelGGL(k_collide_test, dim3(n), dim3(64), 0, st, h->m, n, types, pos, mat, size, margin, out, count);
   HIPCHK(hipGetLastError());
   return AW_OK;
 }

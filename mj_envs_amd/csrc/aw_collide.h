@@ -9,6 +9,7 @@
 // oracle's order.
 #pragma once
 #include "aw_common.h"
+#include "aw_dynamics.h"
 
 namespace aw {
 
@@ -515,13 +516,10 @@ AW_DEV void c_box_box(const GV& A, const GV& B, float margin, Emit& e) {
 // ---------------------------------------------------------------------------------------
 // MPR (libccd ccdMPRPenetration), supports inflated by margin/2 (mjccd_support)
 namespace mpr {
-// Precision (template parameter T, from the kernels' MP parameter): fp64 like MuJoCo's double
-// libccd, or fp32 like libccd's float build -- per task (tasks.py TaskSpec.mpr_fp64),
-// overridable with aw_set_option.  fp32 mis-resolves shallow face-on-face contacts (a cylinder
-// lying on a box face, cm-scale portals whose squared sizes fall under FLT_EPSILON): pen-v0
-// teacher-forced parity 81 % in fp32, 99.9 % in fp64; hammer is as close in fp32 (99.8 %),
-// where fp64 would cost ~5 % of k_step time (fp64 VALU at half the fp32 rate, twice the
-// registers).
+// Run in fp64 (T = double) on fp64 geometry (geom64): MuJoCo's libccd is double, and its contact
+// point on line / face contacts (a cylinder lying on a box) moves between the ends of the line
+// under 1e-7 rad of rotation, i.e. under fp32 kinematics.  (An fp32 path with fp32 inputs measured
+// 81 % teacher-forced parity on pen and 99.4 % on hammer's C3 run; it was removed in round 3.)
 // libccd's CCD_EPS of the matching build: DBL_EPSILON (MuJoCo's double build) / FLT_EPSILON
 template <class T> constexpr T EPS_T = sizeof(T) == 8 ? T(2.220446049250313e-16) : T(1.1920928955078125e-07);
 template <class T> struct GVdT {
@@ -778,31 +776,35 @@ template <class T> AW_DEV int penetration(const Ctx<T>& c, T* depth, T* dir, T* 
 }
 }  // namespace mpr
 
-template <class T>
-AW_DEV void c_convex(const DModel& m, const GV& a, const GV& b, float margin, Emit& e) {
-  // The portal is built in a frame centred on the pair (MPR is translation invariant): support
-  // points are then O(geom size) instead of O(1 m) world coordinates, so every support
-  // evaluation's rounding is ~size * eps instead of ~|x| * eps.  In fp32 that is the difference
-  // between portal jitter of ~3e-8 m and ~1e-9 m on shallow face-on-face contacts whose portals
-  // are ~1e-4 m across.
-  float c[3];
-  mpr::GVdT<T> ad, bd;
-  for (int k = 0; k < 3; k++) {
-    c[k] = 0.5f * (a.pos[k] + b.pos[k]);
-    ad.pos[k] = (T)(a.pos[k] - c[k]); ad.size[k] = a.size[k];
-    bd.pos[k] = (T)(b.pos[k] - c[k]); bd.size[k] = b.size[k];
-  }
-  for (int k = 0; k < 9; k++) { ad.mat[k] = a.mat[k]; bd.mat[k] = b.mat[k]; }
-  ad.type = a.type; bd.type = b.type;
-  mpr::Ctx<T> ctx{&ad, &bd, (T)margin, (T)m.mpr_tolerance, m.mpr_iterations};
-  T depth, dir[3], pos[3];
+// fp64 pose of collidable geom g from the fp64 body frames (stage_kin64), as the oracle's
+// mj_local2Global: geom_xpos = xmat[b] geom_pos + xpos[b], geom_xmat = quat2mat(xquat[b] geom_quat)
+AW_DEV void geom64(const DModel& m, Env& s, int g, mpr::GVdT<double>& G) {
+  const int b = MD(geom_bodyid, g);
+  const double* X = kin64(s, b);
+  double bq[4] = {X[3], X[4], X[5], X[6]}, bm[9], gp[3], gq[4], q[4], sz[3];
+  for (int k = 0; k < 3; k++) { gp[k] = MD(geom_pos64, 3 * g + k); sz[k] = MD(geom_size64, 3 * g + k); }
+  for (int k = 0; k < 4; k++) gq[k] = MD(geom_quat64, 4 * g + k);
+  if (MD(geom_ovr, g)) { apply_ovr64<3>(m, s, 4, g, gp); apply_ovr64<3>(m, s, 5, g, sz); }
+  q2m(bm, bq);
+  mulmv3(G.pos, bm, gp);
+  for (int k = 0; k < 3; k++) { G.pos[k] += X[k]; G.size[k] = sz[k]; }
+  mulq(q, bq, gq);
+  q2m(G.mat, q);
+  G.type = MD(geom_type, g);
+}
+
+// mjc_Convex: MPR in fp64 on fp64 geometry (MuJoCo's double libccd on its double kinematics)
+AW_DEV void c_convex64(const DModel& m, const mpr::GVdT<double>& a, const mpr::GVdT<double>& b, double margin,
+                       Emit& e) {
+  mpr::Ctx<double> ctx{&a, &b, margin, m.mpr_tolerance64, m.mpr_iterations};
+  double depth, dir[3], pos[3];
   if (mpr::penetration(ctx, &depth, dir, pos) != 0) return;
   if (dir[0] == 0 && dir[1] == 0 && dir[2] == 0) return;
-  const float dist = margin - (float)depth;
+  const double dist = margin - depth;
   if (dist > margin) return;
-  const float pf[3] = {(float)pos[0] + c[0], (float)pos[1] + c[1], (float)pos[2] + c[2]};
+  const float pf[3] = {(float)pos[0], (float)pos[1], (float)pos[2]};
   const float df[3] = {(float)dir[0], (float)dir[1], (float)dir[2]};
-  emit(e, dist, pf, df);
+  emit(e, (float)dist, pf, df);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -810,9 +812,17 @@ AW_DEV void c_convex(const DModel& m, const GV& a, const GV& b, float margin, Em
 // 0 plane-*, 1 sphere/capsule pairs, 2 sphere/capsule-box, 3 box-box, 4 anything with a
 // cylinder (MPR).  The class is a template parameter so each class loop carries only its own
 // colliders (no divergent merge of every collider's code and registers).
-template <int C, int MP>
+template <int C>
 AW_DEV void collide_pair(const DModel& m, Env& s, int pair) {
   int g1 = MD(cp_g1, pair), g2 = MD(cp_g2, pair);
+  Emit e{&s, pair, 0};
+  if constexpr (C == 4) {           // every non-plane pair with a cylinder: MPR (mjc_Convex)
+    mpr::GVdT<double> a, b;
+    geom64(m, s, g1, a);
+    geom64(m, s, g2, b);
+    c_convex64(m, a, b, MD(cp_margin64, pair), e);
+    return;
+  }
   GV a, b;
   a.type = MD(geom_type, g1);
   b.type = MD(geom_type, g2);
@@ -827,11 +837,7 @@ AW_DEV void collide_pair(const DModel& m, Env& s, int pair) {
     q2m(a.mat, q1);
     q2m(b.mat, q2);
   }
-  Emit e{&s, pair, 0};
-  if constexpr (C == 4) {           // every non-plane pair with a cylinder: MPR (mjc_Convex)
-    if constexpr (MP) c_convex<double>(m, a, b, margin, e);
-    else c_convex<float>(m, a, b, margin, e);
-  } else if constexpr (C == 0) {
+  if constexpr (C == 0) {
     if (b.type == GEOM_SPHERE) c_plane_sphere(a.pos, a.mat, b.pos, b.size[0], margin, e);
     else if (b.type == GEOM_CAPSULE) c_plane_capsule(a, b, margin, e);
     else if (b.type == GEOM_CYLINDER) c_plane_cylinder(a, b, margin, e);

@@ -49,8 +49,9 @@ enum {
   PR_NEWTON_IT, PR_NOSLIP_IT, PR_NEFC, PR_NCON,
   PR_NT_INIT, PR_NT_HESS, PR_NT_CHOL, PR_NT_SOLVE, PR_NT_LS, PR_NT_UPD, PR_NS_MINV, PR_NS_SETUP, PR_NS_ITER,
   PR_CO_BROAD, PR_CO_NARROW, PR_COM, PR_RNE, PR_CO_C0, PR_CO_C1, PR_CO_C2, PR_CO_C3,
-  PR_NT_HSPARSE, PR_NT_HOFFD, PR_NT_OFFD_ROWS
+  PR_NT_HSPARSE, PR_NT_HOFFD, PR_NT_OFFD_ROWS, PR_CO_KIN64
 };
+static_assert(PR_CO_KIN64 < AW_NPROF, "stage profiler ids");
 #ifdef AW_STAGE_PROF
 #define AW_PROF_START(S)                                            \
   do {                                                              \
@@ -89,8 +90,6 @@ enum {
   DSBL_PASSIVE = 1 << 5, DSBL_GRAVITY = 1 << 6, DSBL_CLAMPCTRL = 1 << 7, DSBL_WARMSTART = 1 << 8,
   DSBL_ACTUATION = 1 << 10, DSBL_REFSAFE = 1 << 11, DSBL_SENSOR = 1 << 12, DSBL_NOSLIP = 1 << 14,
   DSBL_EULERDAMP = 1 << 15,
-  DSBL_MPR_FP64 = 1 << 16,   // ours: run the MPR (cylinder) collider in fp32
-  DSBL_MPR_FP32 = 1 << 17,   // ours: run it in fp64 (neither bit: the task's default)
 };
 enum { ST_BADQPOS = 1, ST_BADQVEL = 2, ST_BADQACC = 4, ST_CON_OVERFLOW = 8, ST_EFC_OVERFLOW = 16 };
 
@@ -152,7 +151,12 @@ constexpr int MAXRG = 64;     // rendered (primitive) geoms
   /* depth renderer: every primitive geom (model order), its collidable index or -1 */        \
   X(int, rg_type, MAXRG) X(int, rg_body, MAXRG) X(int, rg_cgeom, MAXRG)                         \
   X(float, rg_pos, MAXRG * 3) X(float, rg_quat, MAXRG * 4) X(float, rg_size, MAXRG * 3)         \
-  X(float, rg_rbound, MAXRG)
+  X(float, rg_rbound, MAXRG)                                                                   \
+  /* fp64 geometry of the MPR (cylinder) pairs: the model constants of MuJoCo's fp64 kinematics */ \
+  X(double, body_pos64, MAXB * 3) X(double, body_quat64, MAXB * 4) X(double, jnt_pos64, MAXV * 3) \
+  X(double, jnt_axis64, MAXV * 3) X(double, geom_pos64, MAXG * 3) X(double, geom_quat64, MAXG * 4) \
+  X(double, geom_size64, MAXG * 3) X(double, cp_margin64, MAXPAIR)                                 \
+  X(int, body_kin64, MAXB) /* 1: the body's fp64 frame is needed (ancestor of an MPR geom) */
 
 struct MData {
 #define AW_X(T, name, n) T name[n];
@@ -162,11 +166,28 @@ struct MData {
 
 // model read: uniform table base + zero-extended 32-bit byte offset, which maps onto the
 // global_load saddr form (SGPR base, one VGPR offset) instead of a 64-bit per-lane address
+// The table lives in device global memory: reading it through a global-address-space pointer
+// emits global_load (vmcnt only) instead of flat_load, whose completion also holds lgkmcnt and
+// so makes every LDS wait in flight behind it wait for the model read too.
+#ifndef AW_MD_FLAT
+template <class T>
+AW_DEV T mld(const T* base, unsigned i) {
+  typedef const __attribute__((address_space(1))) T GT;
+  typedef const __attribute__((address_space(1))) char GC;
+  return *(GT*)((GC*)base + i * (unsigned)sizeof(T));
+}
+#else
 template <class T>
 AW_DEV T mld(const T* base, unsigned i) {
   return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + i * (unsigned)sizeof(T));
 }
+#endif
 #define MD(name, idx) ::aw::mld(m.d->name, (unsigned)(idx))
+// device-global views of model / state arrays (global_load / global_store, not flat)
+template <class T> using gp_t = __attribute__((address_space(1))) T*;
+template <class T> AW_DEV gp_t<const T> gcp(const T* p) { return (gp_t<const T>)p; }
+template <class T> AW_DEV gp_t<T> gmp(T* p) { return (gp_t<T>)p; }
+#define MDP(name, idx) ::aw::gcp(&m.d->name[idx])
 
 struct DModel {
   int nq, nv, nu, nbody, njnt, ngeom, nsite, ntendon, npairall, nlevel;
@@ -178,6 +199,7 @@ struct DModel {
   int iterations, noslip_iterations, mpr_iterations, disableflags;
   float timestep, gravity[3], tolerance, noslip_tolerance, mpr_tolerance, meaninertia;
   float pen_length, tar_length;
+  double mpr_tolerance64;
   int cls_start[NCLASS + 1];  // collider class c owns pair-list slots [cls_start[c], cls_start[c+1])
   int nrgeom;                 // rendered geoms
   const MData* __restrict__ d;
@@ -251,6 +273,15 @@ struct __attribute__((aligned(16))) Env {
   unsigned long long prof_t;
 #endif
 };
+
+// fp64 body frames of the MPR (cylinder) geometry, stage_kin64 -> narrowphase: [MAXB][8] doubles
+// (xpos[3], xquat[4], pad) in the dense-J storage, dead from kinematics until the constraint rows;
+// its first MAXPAIR shorts hold the broadphase pair list
+constexpr int KIN64_OFF = MAXPAIR * 2;
+static_assert(KIN64_OFF % 16 == 0 && KIN64_OFF + MAXB * 8 * 8 <= JL * VS * 4, "fp64 frames do not fit in the dense-J rows");
+AW_DEV double* kin64(Env& s, int b) {
+  return reinterpret_cast<double*>(reinterpret_cast<char*>(&s.J[0][0]) + KIN64_OFF) + 8 * b;
+}
 
 // ---------------------------------------------------------------------------------------
 // wave primitives
@@ -389,6 +420,29 @@ AW_DEV void mulmtv3(double* r, const double* m, const double* v) {
   double t1 = m[1] * v[0] + m[4] * v[1] + m[7] * v[2];
   double t2 = m[2] * v[0] + m[5] * v[1] + m[8] * v[2];
   r[0] = t0; r[1] = t1; r[2] = t2;
+}
+
+AW_DEV void mulq(double* r, const double* a, const double* b) {
+  double t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  double t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  double t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  double t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
+}
+AW_DEV void rotvq(double* r, const double* v, const double* q) {
+  double u[3] = {q[1], q[2], q[3]}, t[3], t2[3];
+  cross3(t, u, v);
+  scl3(t, t, 2.0);
+  cross3(t2, u, t);
+  r[0] = v[0] + q[0] * t[0] + t2[0];
+  r[1] = v[1] + q[0] * t[1] + t2[1];
+  r[2] = v[2] + q[0] * t[2] + t2[2];
+}
+AW_DEV void q2m(double* m, const double* q) {
+  double w = q[0], x = q[1], y = q[2], z = q[3];
+  m[0] = 1 - 2 * (y * y + z * z); m[1] = 2 * (x * y - w * z); m[2] = 2 * (x * z + w * y);
+  m[3] = 2 * (x * y + w * z); m[4] = 1 - 2 * (x * x + z * z); m[5] = 2 * (y * z - w * x);
+  m[6] = 2 * (x * z - w * y); m[7] = 2 * (y * z + w * x); m[8] = 1 - 2 * (x * x + y * y);
 }
 
 // mju_makeFrame

@@ -147,6 +147,76 @@ AW_DEV void stage_kinematics(const DModel& m, Env& s, int lane) {
   wsync();
 }
 
+template <int N>
+AW_DEV void apply_ovr64(const DModel& m, const Env& s, int field, int obj, double (&v)[N]) {
+  for (int p = 0; p < m.nparam; p++)
+    if (MD(param_field, p) == field && MD(param_obj, p) == obj) {
+      const int c = MD(param_comp, p);
+      const double x = (double)s.prm[p];
+#pragma unroll
+      for (int k = 0; k < N; k++) v[k] = k == c ? x : v[k];
+    }
+}
+
+// mj_kinematics in fp64 for the bodies that carry MPR (cylinder) pair geometry and their
+// ancestors (body_kin64), from the fp32 state with the model's fp64 constants: the oracle's
+// operation order (oracle/mjstep.cc kinematics: parent xmat * body_pos, xquat chain, hinge
+// axis-angle quaternions, normalised).  MPR contact points are ill-conditioned on line / face
+// contacts (a cylinder lying on a box: rotating the cylinder by 1e-7 rad moves MuJoCo's point
+// between the ends), so MPR runs on these fp64 frames, not on the fp32 ones.
+AW_DEV void stage_kin64(const DModel& m, Env& s, int lane) {
+  if (lane == 0) {
+    double* X = kin64(s, 0);
+    X[0] = X[1] = X[2] = 0.0;
+    X[3] = 1.0; X[4] = X[5] = X[6] = 0.0;
+  }
+  wsync();
+  const bool own = lane > 0 && lane < m.nbody && MD(body_kin64, lane);
+  const int b = own ? lane : 0;
+  const int dep = own ? MD(body_depth, b) : -1;
+  const int p = MD(body_parentid, b), da = MD(body_dofadr, b), dn = own ? MD(body_dofnum, b) : 0;
+  double bp[3], bq[4];
+  for (int k = 0; k < 3; k++) bp[k] = MD(body_pos64, 3 * b + k);
+  for (int k = 0; k < 4; k++) bq[k] = MD(body_quat64, 4 * b + k);
+  if (own && MD(body_ovr, b)) { apply_ovr64<3>(m, s, 0, b, bp); apply_ovr64<4>(m, s, 1, b, bq); }
+  for (int lev = 1; lev < m.nlevel; lev++) {
+    if (dep == lev) {
+      const double* P = kin64(s, p);
+      double pq[4] = {P[3], P[4], P[5], P[6]}, pm[9], xp[3], xq[4];
+      q2m(pm, pq);
+      mulmv3(xp, pm, bp);
+      xp[0] += P[0]; xp[1] += P[1]; xp[2] += P[2];
+      mulq(xq, pq, bq);
+      for (int k = 0; k < dn; k++) {
+        const int j = da + k;
+        double axis[3], jp[3], xanchor[3];
+        for (int c = 0; c < 3; c++) { axis[c] = MD(jnt_axis64, 3 * j + c); jp[c] = MD(jnt_pos64, 3 * j + c); }
+        const double q = (double)s.qpos[j];
+        if (MD(jnt_type, j) == JNT_SLIDE) {
+          double xaxis[3];
+          rotvq(xaxis, axis, xq);
+          for (int c = 0; c < 3; c++) xp[c] += xaxis[c] * q;
+        } else {
+          rotvq(xanchor, jp, xq);
+          add3(xanchor, xanchor, xp);
+          double sn, cs, ql[4], v[3];
+          sincos(q * 0.5, &sn, &cs);
+          ql[0] = cs; ql[1] = axis[0] * sn; ql[2] = axis[1] * sn; ql[3] = axis[2] * sn;
+          mulq(xq, xq, ql);
+          rotvq(v, jp, xq);
+          sub3(xp, xanchor, v);
+        }
+      }
+      const double n = sqrt(xq[0] * xq[0] + xq[1] * xq[1] + xq[2] * xq[2] + xq[3] * xq[3]);
+      double* X = kin64(s, b);
+      if (n < 1e-15) { X[3] = 1.0; X[4] = X[5] = X[6] = 0.0; }
+      else for (int c = 0; c < 4; c++) X[3 + c] = xq[c] / n;
+      for (int c = 0; c < 3; c++) X[c] = xp[c];
+    }
+    wsync();
+  }
+}
+
 // mj_comPos: subtree com (divided by the compile-time subtree mass), cinert, cdof
 AW_DEV void stage_com(const DModel& m, Env& s, int lane) {
   for (int b = lane; b < m.nbody; b += 64) {
@@ -167,7 +237,7 @@ AW_DEV void stage_com(const DModel& m, Env& s, int lane) {
     for (int k = 0; k < 4; k++) iq[k] = MD(body_iquat, 4 * b + k);
     mulq(q, s.xquat[b], iq);
     q2m(R, q);
-    const float* I = &m.d->body_inertia[3 * b];
+    const auto I = MDP(body_inertia, 3 * b);
     float mass = s.bmass[b];
     sub3(dif, s.xipos[b], s.subcom[MD(body_rootid, b)]);
     float T[9];
@@ -304,7 +374,7 @@ AW_DEV float stage_velocity(const DModel& m, Env& s, int lane) {
         ctrl = clampf(ctrl, MD(act_ctrlrange, 2 * u), MD(act_ctrlrange, 2 * u + 1));
       float gear = MD(act_gear, u);
       float len = gear * s.qpos[j], vel = gear * s.qvel[j];
-      const float* bp = &m.d->act_bias[3 * u];
+      const auto bp = MDP(act_bias, 3 * u);
       float f = MD(act_gain, u) * ctrl + bp[0] + bp[1] * len + bp[2] * vel;
       if (MD(act_forcelimited, u)) f = clampf(f, MD(act_forcerange, 2 * u), MD(act_forcerange, 2 * u + 1));
       act = gear * f;

@@ -38,6 +38,43 @@ AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
     for (int k = j + 1; k < NV; k++) row[k] = fmaf(-lij, rlane(lij, k), row[k]);
   }
 }
+#elif defined(AW_CHOL_LA)
+// Look-ahead: column j's entries for the next AW_CHOL_LA pivot rows (j+1 .. j+LA) travel by
+// v_readlane (SGPR broadcast) and update those rows at once, so pivot j+1 waits only on this
+// column's readlane, not on the LDS round trip; the rest of the rank-1 update (rows > j+LA) reads
+// the column from LDS as before and lags behind the pivot chain.
+template <int NV>
+AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
+  constexpr int LA = AW_CHOL_LA;
+  float* col = reinterpret_cast<float*>(s.colbuf);
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    const float djj = fmaxf(rlane(row[j], j), MINVAL);
+    const float inv = __builtin_amdgcn_rsqf(djj);
+    const float sq = djj * inv;
+    row[j] = lane == j ? sq : row[j] * inv;
+    if (lane == j) invd = inv;
+    const float lij = row[j];
+#pragma unroll
+    for (int a = 1; a <= LA; a++)
+      if (j + a < NV) row[j + a] = fmaf(-lij, rlane(lij, j + a), row[j + a]);
+    if (j + LA + 1 < NV) {
+      col[lane] = lij;
+      wsync();
+#pragma unroll
+      for (int q = (j + LA + 1) >> 2; q <= (NV - 1) >> 2; q++) {
+        const float4 c = s.colbuf[q];
+        const float cv[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+          const int k = 4 * q + t;
+          if (k > j + LA && k < NV) row[k] = fmaf(-lij, cv[t], row[k]);
+        }
+      }
+      wsync();
+    }
+  }
+}
 #else
 template <int NV>
 AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
@@ -103,7 +140,7 @@ AW_DEV float matvec(const float (&row)[NV], float x) {
 }
 
 // ---------------------------------------------------------------------------------------
-AW_DEV float getimpedance(const float* solimp, float pm) {
+AW_DEV float getimpedance(gp_t<const float> solimp, float pm) {
   float d0 = clampf(solimp[0], 0.0001f, 0.9999f), dmax = clampf(solimp[1], 0.0001f, 0.9999f);
   if (d0 == dmax || solimp[2] <= MINVAL) return 0.5f * (d0 + dmax);
   float x = fabsf(pm / solimp[2]);
@@ -121,8 +158,8 @@ AW_DEV float getimpedance(const float* solimp, float pm) {
 // block.  Spill rows are written and read with VECTOR memory instructions only: every read
 // below uses a lane-dependent address (a row per lane, or the row's entry per lane followed by
 // a readlane broadcast), so no uniform (scalar-cache) load can see a previous substep's row.
-AW_DEV float* jspill_row(const DModel& m, const Env& s, int d) {
-  return m.jspill + (size_t)s.slot * JSPILL + (size_t)(d - JL) * VS;
+AW_DEV gp_t<float> jspill_row(const DModel& m, const Env& s, int d) {
+  return gmp(m.jspill) + (size_t)s.slot * JSPILL + (size_t)(d - JL) * VS;
 }
 AW_DEV void jput(const DModel& m, Env& s, int d, int k, float v) {
   if (d < JL) s.J[d][k] = v;
@@ -137,22 +174,23 @@ AW_DEV void jspill_fence() {
 // The smooth solve's factor of M is needed again by noslip (inv(M)) after Newton has reused the
 // LDS factor storage: it is parked in this env's global block (L2-resident, 16-byte vector
 // stores / loads, lane-dependent addresses) instead of refactoring M.
-AW_DEV float4* msave_block(const DModel& m, const Env& s) {
-  return reinterpret_cast<float4*>(m.msave + (size_t)s.slot * NPACK_SAVE);
+typedef float f4v __attribute__((ext_vector_type(4)));
+AW_DEV gp_t<f4v> msave_block(const DModel& m, const Env& s) {
+  return (gp_t<f4v>)(gmp(m.msave) + (size_t)s.slot * NPACK_SAVE);
 }
 template <int NV>
 AW_DEV void msave_store(const DModel& m, const Env& s, int lane) {
   constexpr int n4 = (tri(NV) + 3) / 4;
-  float4* dst = msave_block(m, s);
-  const float4* src = reinterpret_cast<const float4*>(s.L);
+  gp_t<f4v> dst = msave_block(m, s);
+  const f4v* src = reinterpret_cast<const f4v*>(s.L);
   for (int i = lane; i < n4; i += 64) dst[i] = src[i];
 }
 template <int NV>
 AW_DEV void msave_load(const DModel& m, Env& s, int lane) {
   constexpr int n4 = (tri(NV) + 3) / 4;
   jspill_fence();   // the stores of msave_store (same wave) are complete
-  const float4* src = msave_block(m, s);
-  float4* dst = reinterpret_cast<float4*>(s.L);
+  gp_t<const f4v> src = msave_block(m, s);
+  f4v* dst = reinterpret_cast<f4v*>(s.L);
   for (int i = lane; i < n4; i += 64) dst[i] = src[i];
 }
 
@@ -170,7 +208,7 @@ AW_DEV float row_dot(const DModel& m, const Env& s, int r, const float* x) {
 #pragma unroll
     for (int k = 0; k < NV; k++) acc = fmaf(J[k], x[k], acc);
   } else {
-    const float* J = jspill_row(m, s, d);
+    gp_t<const float> J = jspill_row(m, s, d);
 #pragma unroll
     for (int k = 0; k < NV; k++) acc = fmaf(J[k], x[k], acc);
   }
@@ -196,7 +234,7 @@ AW_DEV float jt_mul(const DModel& m, Env& s, int lane) {
   const int nd = s.ndense, ndl = nd < JL ? nd : JL;
   for (int d = 0; d < ndl; d++) out = fmaf(s.J[d][li], s.rowbuf[s.nsparse + d], out);
   if (nd > JL) {
-    const float* Jg = jspill_row(m, s, JL);
+    gp_t<const float> Jg = jspill_row(m, s, JL);
     for (int d = JL; d < nd; d++, Jg += VS) out = fmaf(Jg[li], s.rowbuf[s.nsparse + d], out);
   }
   return lane < NV ? out : 0.f;
@@ -376,11 +414,11 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
   // impedance, regularisation, reference acceleration
   for (int r = lane; r < s.nefc; r += 64) {
     int t = s.efc_type[r], id = s.efc_id[r];
-    const float *solref, *solimp;
-    if (t == C_FRIC_DOF) { solref = &m.d->dof_solref[2 * id]; solimp = &m.d->dof_solimp[5 * id]; }
-    else if (t == C_LIM_JNT) { solref = &m.d->jnt_solref[2 * id]; solimp = &m.d->jnt_solimp[5 * id]; }
-    else if (t == C_LIM_TEN) { solref = &m.d->ten_solref[2 * id]; solimp = &m.d->ten_solimp[5 * id]; }
-    else { int pr = s.con_pair[id]; solref = &m.d->cp_solref[2 * pr]; solimp = &m.d->cp_solimp[5 * pr]; }
+    gp_t<const float> solref, solimp;
+    if (t == C_FRIC_DOF) { solref = MDP(dof_solref, 2 * id); solimp = MDP(dof_solimp, 5 * id); }
+    else if (t == C_LIM_JNT) { solref = MDP(jnt_solref, 2 * id); solimp = MDP(jnt_solimp, 5 * id); }
+    else if (t == C_LIM_TEN) { solref = MDP(ten_solref, 2 * id); solimp = MDP(ten_solimp, 5 * id); }
+    else { int pr = s.con_pair[id]; solref = MDP(cp_solref, 2 * pr); solimp = MDP(cp_solimp, 5 * pr); }
     float pm = s.rowbuf[r];          // stashed by the row assembly above
     float imp = getimpedance(solimp, pm);
     float dmax = clampf(solimp[1], 0.0001f, 0.9999f);
@@ -416,10 +454,13 @@ constexpr int NSP_CACHE = AW_NSP_CACHE;   // noslip edge pairs whose jd / xd row
 constexpr int XPS = 2 * MAXV;
 constexpr int NSP_UNION = (int)(offsetof(Env, qpos) / (XPS * sizeof(float)));
 constexpr int NSP_ROWS = MAXEFC / XPS;          // slots in each of efc_D and rowbuf
-constexpr int NSP_LDS = NSP_UNION + 2 * NSP_ROWS;
+// KEEP_D (aw_forward_dump's k_dump): efc_D is reported after the solve, so it is not parked in
+template <bool KEEP_D> constexpr int NSP_LDS = NSP_UNION + (KEEP_D ? 1 : 2) * NSP_ROWS;
+template <bool KEEP_D>
 AW_DEV float* xpark_slot(Env& s, int q) {
   if (q < NSP_UNION) return reinterpret_cast<float*>(&s) + q * XPS;
   q -= NSP_UNION;
+  if (KEEP_D) return s.rowbuf + q * XPS;
   return q < NSP_ROWS ? s.efc_D + q * XPS : s.rowbuf + (q - NSP_ROWS) * XPS;
 }
 struct RowR {
@@ -464,7 +505,7 @@ AW_DEV void hess_dense_mfma(const DModel& m, Env& s, int lane) {
     if (__ballot(w != 0.f) == 0ull) continue;
     const int dd = d < nd ? d : nd - 1;
     // JL is a multiple of 4: a K-step's rows are all in LDS or all in the spill block
-    const float* Jr = d0 < JL ? &s.J[dd][0] : jspill_row(m, s, dd);
+    const float* Jr = d0 < JL ? &s.J[dd][0] : (const float*)jspill_row(m, s, dd);
     float b0 = Jr[col], b1 = Jr[16 + col];
     b0 = w != 0.f ? b0 : 0.f;
     b1 = (w != 0.f && 16 + col < NV) ? b1 : 0.f;
@@ -478,7 +519,7 @@ AW_DEV void hess_dense_mfma(const DModel& m, Env& s, int lane) {
         if (dq >= nd) break;
         const float wq = s.rowbuf[ns + dq];
         if (wq == 0.f) continue;
-        const float* Jq = d0 < JL ? &s.J[dq][0] : jspill_row(m, s, dq);
+        const float* Jq = d0 < JL ? &s.J[dq][0] : (const float*)jspill_row(m, s, dq);
         const float jl = Jq[li];
         const float av = wq * jl;
 #pragma unroll
@@ -722,7 +763,7 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
     }
     if (nd > JL) {
       // spill rows: the row's entry per lane (coalesced), broadcast with readlane
-      const float* Jg = jspill_row(m, s, JL);
+      gp_t<const float> Jg = jspill_row(m, s, JL);
       for (int d = JL; d < nd; d++, Jg += VS) {
         float w = s.rowbuf[s.nsparse + d];
         if (w == 0.f) continue;
@@ -818,7 +859,7 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
 
 // ---------------------------------------------------------------------------------------
 // noslip: PGS over frictionloss rows and opposing pyramid-edge pairs, no regularisation
-template <int NV>
+template <int NV, bool KEEP_D>
 AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[NV], float& qacc) {
   const int nsparse = s.nsparse, ndense = s.ndense;
   // inv(M): factor, then lane i solves M x = e_i (multi-RHS, L entries broadcast from LDS);
@@ -911,6 +952,9 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
   // are parked in dead LDS, the rest are rebuilt each sweep.
   int npr = 0, pr_e = 0;
   float pr_k = 0.f, pr_ik = 0.f, pr_ard = 0.f;
+#ifdef AW_NS_BLOCK
+  float pc1 = 0.f, pc2 = 0.f, pc3 = 0.f;   // lane p: jd_p . xd_p-1, xd_p-2, xd_p-3 within p's block
+#endif
   float c_jd[NSP_CACHE], c_xd[NSP_CACHE];
 #pragma unroll
   for (int p = 0; p < NSP_CACHE; p++) c_jd[p] = c_xd[p] = 0.f;
@@ -944,12 +988,28 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
       pr_e = e; pr_k = K; pr_ik = 1.0f / K;
       pr_ard = s.efc_aref[nsparse + e] - s.efc_aref[nsparse + e + 1];
     }
+#ifdef AW_NS_BLOCK
+    // couplings jd_p . xd_p-k to the earlier pairs of p's block of 4 (blocked Gauss-Seidel below)
+    if (p < NSP_CACHE && (p & 3)) {
+      float x1 = 0.f, x2 = 0.f, x3 = 0.f;
+#pragma unroll
+      for (int q = 0; q < NSP_CACHE; q++) {
+        x1 = q == p - 1 ? c_xd[q] : x1;
+        x2 = q == p - 2 ? c_xd[q] : x2;
+        x3 = q == p - 3 ? c_xd[q] : x3;
+      }
+      const float k1 = wave_sum(jd * x1);
+      const float k2 = (p & 3) >= 2 ? wave_sum(jd * x2) : 0.f;
+      const float k3 = (p & 3) >= 3 ? wave_sum(jd * x3) : 0.f;
+      if (lane == p) { pc1 = k1; pc2 = k2; pc3 = k3; }
+    }
+#endif
 #pragma unroll
     for (int q = 0; q < NSP_CACHE; q++)
       if (q == p) { c_jd[q] = jd; c_xd[q] = xd; }
 #ifndef AW_NOSLIP_NOLDS
-    if (p >= NSP_CACHE && p < NSP_CACHE + NSP_LDS && lane < MAXV) {
-      float* slot = xpark_slot(s, p - NSP_CACHE);
+    if (p >= NSP_CACHE && p < NSP_CACHE + NSP_LDS<KEEP_D> && lane < MAXV) {
+      float* slot = xpark_slot<KEEP_D>(s, p - NSP_CACHE);
       slot[lane] = jd;
       slot[MAXV + lane] = xd;
     }
@@ -1019,14 +1079,53 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
         if (lane + 64 == e + 1) fd_hi = f2n;
       }
     };
+#ifdef AW_NS_BLOCK
+    // Blocked Gauss-Seidel over the cached pairs, four at a time: the four residual sums
+    // jd_p . qacc are taken at once against the block's starting qacc (independent reductions
+    // that overlap), and pair p's sum is then corrected by the couplings jd_p . xd_q to the
+    // block's earlier pairs q times their updates d_q -- the same sweep as one pair at a time
+    // (r_p = jd_p . (qacc + sum_q xd_q d_q)), with one reduction latency per block on the chain.
+    auto pair_upd = [&](int p, float sq) {
+      const int e = rlane_i(pr_e, p);
+      const float f1 = fd_get(e), f2 = fd_get(e + 1);
+      const float ik = rlane(pr_ik, p), ard = rlane(pr_ard, p);
+      const float d1 = __builtin_amdgcn_fmed3f(fmaf(-sq, ik, ard * ik), -f1, f2);
+      const float rd = sq - ard;
+      const float f1n = f1 + d1, f2n = f2 - d1;
+      impr -= rd * d1 + 0.5f * rlane(pr_k, p) * d1 * d1;
+      if (e < 64) {
+        if (lane == e) fd = f1n;
+        if (lane == e + 1) fd = f2n;
+        if (e == 63 && lane == 0) fd_hi = f2n;
+      } else {
+        if (lane + 64 == e) fd_hi = f1n;
+        if (lane + 64 == e + 1) fd_hi = f2n;
+      }
+      return d1;
+    };
+#pragma unroll
+    for (int b = 0; b < NSP_CACHE; b += 4) {
+      if (b < npr) {
+        const float s0 = wave_sum(c_jd[b] * qacc), s1 = wave_sum(c_jd[b + 1] * qacc);
+        const float s2 = wave_sum(c_jd[b + 2] * qacc), s3 = wave_sum(c_jd[b + 3] * qacc);
+        const float d0 = pair_upd(b, s0);
+        const float d1 = pair_upd(b + 1, fmaf(rlane(pc1, b + 1), d0, s1));
+        const float d2 = pair_upd(b + 2, fmaf(rlane(pc1, b + 2), d1, fmaf(rlane(pc2, b + 2), d0, s2)));
+        const float d3 = pair_upd(b + 3, fmaf(rlane(pc1, b + 3), d2, fmaf(rlane(pc2, b + 3), d1,
+                                                                       fmaf(rlane(pc3, b + 3), d0, s3))));
+        qacc = fmaf(c_xd[b], d0, fmaf(c_xd[b + 1], d1, fmaf(c_xd[b + 2], d2, fmaf(c_xd[b + 3], d3, qacc))));
+      }
+    }
+#else
 #pragma unroll
     for (int p = 0; p < NSP_CACHE; p++)
       if (p < npr) pair_step(p, c_jd[p], c_xd[p]);
+#endif
     for (int p = NSP_CACHE; p < npr; p++) {
       float jd, xd;
 #ifndef AW_NOSLIP_NOLDS
-      if (p < NSP_CACHE + NSP_LDS) {   // parked in LDS
-        const float* slot = xpark_slot(s, p - NSP_CACHE);
+      if (p < NSP_CACHE + NSP_LDS<KEEP_D>) {   // parked in LDS
+        const float* slot = xpark_slot<KEEP_D>(s, p - NSP_CACHE);
         jd = lane < MAXV ? slot[lane] : 0.f;
         xd = lane < MAXV ? slot[MAXV + lane] : 0.f;
       } else
@@ -1118,7 +1217,8 @@ AW_DEV void stage_touch(const DModel& m, Env& s, int lane) {
           copy3(ray, s.con_nrm[lane]);
           normalize3(ray);
           if (bid == b2) scl3(ray, ray, -1.f);
-          if (ray_geom(s.sxpos[site], s.txmat[t], &m.d->touch_size[3 * t], s.con_pos[lane], ray, MD(touch_type, t)) >= 0.f)
+          float tsz[3] = {MD(touch_size, 3 * t), MD(touch_size, 3 * t + 1), MD(touch_size, 3 * t + 2)};
+          if (ray_geom(s.sxpos[site], s.txmat[t], tsz, s.con_pos[lane], ray, MD(touch_type, t)) >= 0.f)
             val = fn;
         }
       }

@@ -164,6 +164,47 @@ def test_global_offset_changes_streams():
     assert not torch.equal(pa, pb) and not torch.equal(xa, xb)
 
 
+def test_checkpoint_resume_bitwise():
+    """The checkpoint contract of include/adroit_wave.h: aw_get_state + aw_get_episode +
+    aw_episode_totals saved mid-run and restored into a NEW handle (aw_set_state, aw_set_episode,
+    aw_set_episode_totals) continue the run bit for bit -- auto-resets (Philox keyed by the
+    finished-episode count) and the running totals (count, summed return, successes) included."""
+    env_id, n, seed = "pen-v0", 128, 31
+    _, a = _sim(env_id, n)
+    _, b = _sim(env_id, n)
+    act = a.empty(n, a.nu)
+    bufs_a, bufs_b = _bufs(a, n), _bufs(b, n)
+    a.reset(bufs_a[0], seed=seed)
+
+    def run(s, bufs, k0, k1):
+        for k in range(k0, k1):
+            s.random_actions(act, 9, k)
+            s.step(act, *bufs, autoreset=True, seed=seed)
+
+    def totals(s):
+        e, r, c = s.empty(n, dtype=torch.int32), s.empty(n), s.empty(n, dtype=torch.int32)
+        s.episode_totals(e, r, c)
+        return e, r, c
+
+    run(a, bufs_a, 0, 150)                       # pen horizon 100: every env has reset once
+    q, v, w, p = a.empty(n, a.nq), a.empty(n, a.nv), a.empty(n, a.nv), a.empty(n, a.nparam)
+    a.get_state(q, v, w, p)
+    el, er, eg = a.empty(n, dtype=torch.int32), a.empty(n), a.empty(n, dtype=torch.int32)
+    a.get_episode(el, er, eg)
+    te, tr, ts = totals(a)
+    b.set_state(q, v, w, p, obs=bufs_b[0])
+    b.set_episode(el, er, eg)
+    b.set_episode_totals(te, tr, ts)
+    run(a, bufs_a, 150, 320)
+    run(b, bufs_b, 150, 320)
+    ta, tb = totals(a), totals(b)
+    torch.cuda.synchronize()
+    assert int(te.min()) >= 1 and int(ta[0].min()) >= 3
+    assert torch.equal(bufs_a[0], bufs_b[0])
+    for x, y in zip(ta, tb):
+        assert torch.equal(x, y)
+
+
 # --------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("field", ["qvel", "qpos"])
 def test_nan_state_flags_and_resets_like_oracle(field):
@@ -173,11 +214,13 @@ def test_nan_state_flags_and_resets_like_oracle(field):
     from mj_envs_amd.tasks import sample_params
     env_id, n = "hammer-v0", 8
     m, o = make_oracle(env_id)
-    P = sample_params(env_id, m, np.random.default_rng(2), n)
+    P = sample_params(env_id, m, np.random.default_rng(2), n).astype(np.float32).astype(np.float64)
     st, _ = o.reset(P)
     rng = np.random.default_rng(3)
     for _ in range(5):
         o.step(st, rng.uniform(-1, 1, (n, o.nu)), nthreads=8)
+    for k in ("qpos", "qvel", "warm"):   # the GPU's fp32 state, for both sides
+        st[k] = st[k].astype(np.float32).astype(np.float64)
     bad = [1, 5]
     for e in bad:
         st[field][e, 3] = np.nan

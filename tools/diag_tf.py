@@ -48,7 +48,7 @@ def main(env_id="hammer-v0", pol_kind="dapg", steps=80, n=64, max_cases=12, dsbl
         sim.set_option(disableflags=dsbl)
         one.set_option(disableflags=dsbl)
         o.set_option(disableflags=dsbl & 0xFFFF)
-    P = sample_params(env_id, m, np.random.default_rng(11), n, variation)
+    P = sample_params(env_id, m, np.random.default_rng(11), n, variation).astype(np.float32).astype(np.float64)
     obs = sim.empty(n, sim.obs_dim)
     t = lambda a: torch.tensor(np.asarray(a), dtype=torch.float32, device="cuda")
     sim.reset(obs, params=t(P))
@@ -77,11 +77,25 @@ def main(env_id="hammer-v0", pol_kind="dapg", steps=80, n=64, max_cases=12, dsbl
                           float(np.abs(qg[e] - st["qpos"][e]).max()), float(np.abs(vg[e] - st["qvel"][e]).max())))
     print(f"{env_id} {pol_kind}: {len(cases)} of {n * steps} cases outside tolerance", flush=True)
     report = []
-    for (k, e, pre, a, dq, dv) in cases[:max_cases]:
+    # one case per distinct step first (the misses of one step are often one replicated state),
+    # then the remaining ones in order
+    seen, pick, rest = set(), [], []
+    for c in cases:
+        (rest if c[0] in seen else pick).append(c)
+        seen.add(c[0])
+    hist = {}
+    for c in cases:
+        hist[c[0]] = hist.get(c[0], 0) + 1
+    print("misses per step:", sorted(hist.items(), key=lambda x: -x[1])[:20], flush=True)
+    for (k, e, pre, a, dq, dv) in (pick + rest)[:max_cases]:
         ctrl = m.task_act_mid + np.clip(a, -1, 1) * m.task_act_rng
         qp, qv, wm = pre["qpos"].copy(), pre["qvel"].copy(), pre["warm"].copy()
-        rec = dict(step=k, env=e, dqpos=dq, dqvel=dv, substeps=[])
+        rec = dict(step=k, env=e, dqpos=dq, dqvel=dv, substeps=[],
+                   pre=dict(qpos=pre["qpos"].tolist(), qvel=pre["qvel"].tolist(), warm=pre["warm"].tolist(),
+                            params=np.asarray(pre["params"]).tolist(), action=np.asarray(a).tolist()))
         for j in range(sim.frame_skip):
+            # both sides start the substep from the same (fp32-representable) state
+            qp, qv, wm = (x.astype(np.float32).astype(np.float64) for x in (qp, qv, wm))
             o.forward1(pre["params"], qp, qv, wm, ctrl)
             sc = o.get("scalars")
             oc = o.get("contact").reshape(-1, 23)
@@ -118,8 +132,15 @@ def main(env_id="hammer-v0", pol_kind="dapg", steps=80, n=64, max_cases=12, dsbl
                                    force=rel(d["efc_force"][:ne], of),
                                    worst_force_rows=[(int(r), int(d["efc_type"][r]), float(d["efc_force"][r]),
                                                       float(of[r])) for r in np.argsort(-np.abs(d["efc_force"][:ne] - of))[:4]])
+                sub["state"] = dict(qpos=qp.tolist(), qvel=qv.tolist(), warm=wm.tolist(), ctrl=np.asarray(ctrl).tolist())
                 if len(oc):
                     sub["contact_pos_err"] = float(np.abs(d["con_pos"] - oc[:, 1:4]).max())
+                    pe = np.abs(d["con_pos"] - oc[:, 1:4]).max(axis=1)
+                    sub["pos_err_by_contact"] = [
+                        dict(pair=gname(m, int(c[13])) + "|" + gname(m, int(c[14])), idx=int(i), err=round(float(pe[i]), 6),
+                             gpu=[round(float(x), 6) for x in d["con_pos"][i]], oracle=[round(float(x), 6) for x in c[1:4]],
+                             dist_gpu=float(d["con_dist"][i]), dist_oracle=float(c[0]))
+                        for i, c in enumerate(oc)]
                     fe = np.abs(d["con_frame"] - oc[:, 4:13]).max(axis=1)
                     sub["contact_frame_err"] = float(fe.max())
                     sub["frame_err_by_contact"] = [(gname(m, int(c[13])) + "|" + gname(m, int(c[14])), round(float(e), 5),
@@ -136,7 +157,8 @@ def main(env_id="hammer-v0", pol_kind="dapg", steps=80, n=64, max_cases=12, dsbl
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     tag = f"{env_id.split('-')[0]}_{pol_kind}" + (f"_{variation}" if variation else "") + (f"_{dsbl:#x}" if dsbl else "")
     with open(os.path.join(REPO, "gpurun_out", f"diag_{tag}.json"), "w") as f:
-        json.dump(dict(env_id=env_id, policy=pol_kind, n=n, steps=steps, misses=len(cases), cases=report), f, indent=1)
+        json.dump(dict(env_id=env_id, policy=pol_kind, n=n, steps=steps, misses=len(cases),
+                       misses_per_step={int(k): v for k, v in sorted(hist.items())}, cases=report), f, indent=1)
 
 
 if __name__ == "__main__":
