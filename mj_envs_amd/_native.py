@@ -67,7 +67,6 @@ def load():
     L.aw_episode_totals.argtypes = [_vp, _vp, _vp, _vp, _vp]
     L.aw_get_episode.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp]
     L.aw_set_episode.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp]
-    L.aw_set_episode_totals.argtypes = [_vp, _vp, _vp, _vp, _vp]
     L.aw_get_state.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp]
     L.aw_set_state.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp]
     L.aw_status.argtypes = [_vp, _vp, _vp, _vp]
@@ -79,6 +78,9 @@ def load():
     L.aw_collide_test.restype = ctypes.c_int
     # (diagnostic builds of older revisions, selected with AW_LIB, may lack the newer entry points;
     # calling one of those then raises AttributeError)
+    if hasattr(L, "aw_set_episode_totals"):
+        L.aw_set_episode_totals.argtypes = [_vp, _vp, _vp, _vp, _vp]
+        L.aw_set_episode_totals.restype = ctypes.c_int
     if hasattr(L, "aw_render_depth"):
         L.aw_render_depth.argtypes = [_vp, _vp, ctypes.c_int, ctypes.c_int, _vp, _vp]
         L.aw_render_depth.restype = ctypes.c_int
@@ -89,7 +91,7 @@ def load():
     for f in ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "aw_step",
               "aw_random_actions", "aw_get_state", "aw_set_state", "aw_status", "aw_episode_stats",
               "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_set_env_offset", "aw_clear_status",
-              "aw_episode_totals", "aw_get_episode", "aw_set_episode", "aw_set_episode_totals"):
+              "aw_episode_totals", "aw_get_episode", "aw_set_episode"):
         getattr(L, f).restype = ctypes.c_int
     _lib = L
     return L

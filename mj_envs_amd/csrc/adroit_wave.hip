@@ -22,6 +22,7 @@
 #include "aw_policy.h"
 #include "aw_solver.h"
 #include "aw_task.h"
+#include "aw_tree.h"
 
 using namespace aw;
 
@@ -150,8 +151,9 @@ struct Dof {
 // mj_forward: everything up to qacc / forces / sensors; Mrow is left in registers.  Stage order
 // follows the LDS overlays (aw_common.h Env): the constraint rows are assembled while the
 // phase-K arrays (cdof, subcom) are alive, then the solver phase reuses that storage.
-template <int NV, bool KEEP_D = false>
-AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV], Dof& d) {
+template <int TASK, bool KEEP_D = false>
+AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[Tree<TASK>::NV], Dof& d) {
+  constexpr int NV = Tree<TASK>::NV;
   stage_kinematics(m, s, lane);
   AW_PROF(s, PR_KIN);
   stage_collision(m, s, lane);
@@ -165,19 +167,14 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV], Dof& d
   if (lane == 0) { s.it_newton = 0; s.it_noslip = 0; }
   stage_constraints<NV>(m, s, lane);
   AW_PROF(s, PR_CONSTR);
-  // qacc_smooth = M \ qfrc_smooth
+  // qacc_smooth = M \ qfrc_smooth: mj_factorM + mj_solveM over the dof tree (aw_tree.h)
   {
     float row[NV];
 #pragma unroll
     for (int k = 0; k < NV; k++) row[k] = Mrow[k];
-    float invd = 1.f;
-    chol_factor<NV>(row, lane, invd, s);
-    chol_store<NV>(row, lane, s);
-    wsync();
-#ifndef AW_NOSLIP_REFACTOR
-    if (s.nefc > 0 && m.noslip_iterations > 0 && !(m.disableflags & DSBL_NOSLIP)) msave_store<NV>(m, s, lane);
-#endif
-    d.qacc_smooth = chol_solve<NV>(row, invd, lane < NV ? d.qfrc_smooth : 0.f, lane, s);
+    float invd;
+    tree_factor<TASK>(row, invd, lane);
+    d.qacc_smooth = tree_solve<TASK>(row, invd, d.qfrc_smooth, lane);
   }
   AW_PROF(s, PR_SMOOTH);
   if (s.nefc == 0) {
@@ -187,7 +184,7 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV], Dof& d
     float a = 0.f;
     solve_newton<NV>(m, s, lane, Mrow, a, d.qfrc_smooth, d.qacc_smooth);
     AW_PROF(s, PR_NEWTON);
-    if (m.noslip_iterations > 0 && !(m.disableflags & DSBL_NOSLIP)) solve_noslip<NV, KEEP_D>(m, s, lane, Mrow, a);
+    if (m.noslip_iterations > 0 && !(m.disableflags & DSBL_NOSLIP)) solve_noslip<TASK, KEEP_D>(m, s, lane, Mrow, a);
     AW_PROF(s, PR_NOSLIP);
     for (int r = lane; r < s.nefc; r += 64) s.rowbuf[r] = s.efc_force[r];
     wsync();
@@ -199,9 +196,11 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[NV], Dof& d
   AW_PROF(s, PR_JT_TOUCH);
 }
 
-// mj_Euler: implicit joint damping, semi-implicit positions, warmstart <- qacc
-template <int NV>
-AW_DEV void euler(const DModel& m, Env& s, int lane, const float (&Mrow)[NV], const Dof& d) {
+// mj_Euler: implicit joint damping (M + h D factored over the dof tree, aw_tree.h),
+// semi-implicit positions, warmstart <- qacc
+template <int TASK>
+AW_DEV void euler(const DModel& m, Env& s, int lane, const float (&Mrow)[Tree<TASK>::NV], const Dof& d) {
+  constexpr int NV = Tree<TASK>::NV;
   const float h = m.timestep;
   const bool dmp = !(m.disableflags & (DSBL_EULERDAMP | DSBL_PASSIVE));
   float acc;
@@ -210,12 +209,9 @@ AW_DEV void euler(const DModel& m, Env& s, int lane, const float (&Mrow)[NV], co
     const float dd = lane < NV ? h * MD(dof_damping, lane) : 0.f;
 #pragma unroll
     for (int k = 0; k < NV; k++) row[k] = Mrow[k] + (k == lane ? dd : 0.f);
-    float invd = 1.f;
-    chol_factor<NV>(row, lane, invd, s);
-    chol_store<NV>(row, lane, s);
-    wsync();
-    float f = lane < NV ? d.qfrc_smooth + d.qfrc_con : 0.f;
-    acc = chol_solve<NV>(row, invd, f, lane, s);
+    float invd;
+    tree_factor<TASK>(row, invd, lane);
+    acc = tree_solve<TASK>(row, invd, d.qfrc_smooth + d.qfrc_con, lane);
   } else {
     acc = d.qacc;
   }
@@ -315,13 +311,14 @@ AW_DEV void reset_prepare(const DModel& m, Env& s, const DState& st, int env, in
 }
 
 // reset one env in LDS: params (given or sampled), qpos0/0/0, forward, obs
-template <int NV>
+template <int TASK>
 AW_DEV void reset_env(const DModel& m, Env& s, const DState& st, int env, int lane,
                       const float* params_in, uint64_t seed, float* obs) {
+  constexpr int NV = Tree<TASK>::NV;
   reset_prepare<NV>(m, s, st, env, lane, params_in, seed);
   float Mrow[NV];
   Dof d;
-  forward<NV>(m, s, lane, Mrow, d);
+  forward<TASK>(m, s, lane, Mrow, d);
   if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
 }
 
@@ -329,12 +326,13 @@ AW_DEV void reset_env(const DModel& m, Env& s, const DState& st, int env, int la
 // in-kernel auto-reset.  forward<NV> has exactly ONE inlined call site (the loop below drives
 // substeps, the mj_checkAcc retry and the reset forward through it), which keeps the code
 // object small enough for the instruction cache.
-template <int NV>
+template <int TASK>
 __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DModel* __restrict__ mptr, DState stval,
                                              int n, const float* __restrict__ actions,
                                              float* obs, float* reward, uint8_t* done, uint8_t* goal,
                                              float* terminal_obs, int autoreset, uint64_t seed,
                                              int* __restrict__ next_env) {
+  constexpr int NV = Tree<TASK>::NV;
 #ifndef AW_MODEL_BYVAL
   // model scalars read from the device copy on demand (scalar loads behind the loop's memory
   // clobber) instead of ~50 kernel-argument SGPRs held live across the whole launch
@@ -376,13 +374,21 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
       // memory clobber: keeps LICM from hoisting the (loop-invariant) model loads of a whole
       // substep out of this loop, which would pin them in registers across every stage
       asm volatile("" ::: "memory");
-      if (!resetting && !retry) check_state<NV>(s, lane);
+#ifndef AW_NO_OPAQUE_LANE
+      // and no lane-dependent value is hoisted out of the loop either (the lane id is re-derived
+      // per substep): loop-invariant masks and offsets would otherwise occupy SGPRs / VGPRs across
+      // every stage of the substep
+      const int sl = opaque(lane);
+#else
+      const int sl = lane;
+#endif
+      if (!resetting && !retry) check_state<NV>(s, sl);
       AW_PROF(s, PR_CHECK);
-      forward<NV>(m, s, lane, Mrow, d);
+      forward<TASK>(m, s, sl, Mrow, d);
       if (resetting) break;
-      if (!retry && check_acc<NV>(s, lane, d)) { retry = true; continue; }
+      if (!retry && check_acc<NV>(s, sl, d)) { retry = true; continue; }
       retry = false;
-      euler<NV>(m, s, lane, Mrow, d);
+      euler<TASK>(m, s, sl, Mrow, d);
       AW_PROF(s, PR_EULER);
       AW_PROF_COUNT(s, PR_SUBSTEPS);
       if (++sub < m.frame_skip) continue;
@@ -445,23 +451,25 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
   }
 }
 
-template <int NV>
+template <int TASK>
 __global__ void __launch_bounds__(64) k_reset(DModel m, DState st, int n, const uint8_t* mask,
                                               const float* params, uint64_t seed, float* obs) {
+  constexpr int NV = Tree<TASK>::NV;
   __shared__ Env s;
   const int env = blockIdx.x, lane = threadIdx.x;
   if (env >= n) return;
   if (mask && !mask[env]) return;
   if (lane == 0) { s.status = 0u; s.slot = blockIdx.x; }
-  reset_env<NV>(m, s, st, env, lane, params, seed, obs);
+  reset_env<TASK>(m, s, st, env, lane, params, seed, obs);
   store_env<NV>(m, s, st, env, lane);
   if (lane == 0) { st.status[env] = s.status; st.status_acc[env] |= s.status; }
 }
 
-template <int NV>
+template <int TASK>
 __global__ void __launch_bounds__(64) k_set_state(DModel m, DState st, int n, const float* qpos,
                                                   const float* qvel, const float* warm,
                                                   const float* params, float* obs) {
+  constexpr int NV = Tree<TASK>::NV;
   __shared__ Env s;
   const int env = blockIdx.x, lane = threadIdx.x;
   if (env >= n) return;
@@ -478,7 +486,7 @@ __global__ void __launch_bounds__(64) k_set_state(DModel m, DState st, int n, co
   stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
   float Mrow[NV];
   Dof d;
-  forward<NV>(m, s, lane, Mrow, d);
+  forward<TASK>(m, s, lane, Mrow, d);
   if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
   store_env<NV>(m, s, st, env, lane);
   if (lane == 0) { st.status[env] = s.status; st.status_acc[env] |= s.status; }
@@ -487,8 +495,9 @@ __global__ void __launch_bounds__(64) k_set_state(DModel m, DState st, int n, co
 // dump layout (floats): see mj_envs_amd/_native.py dump_layout (same offsets from the capacities)
 constexpr int DUMP_SCAL = 1760, DUMP_CON = 1768, DUMP_EFC = DUMP_CON + 14 * MAXCON;
 static_assert(DUMP_EFC + 4 * MAXEFC == AW_DUMP_SIZE, "AW_DUMP_SIZE out of date");
-template <int NV>
+template <int TASK>
 __global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const float* ctrl, float* out) {
+  constexpr int NV = Tree<TASK>::NV;
   __shared__ Env s;
   const int lane = threadIdx.x;
   load_env<NV>(m, s, st, env, lane);
@@ -496,7 +505,7 @@ __global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const
   stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
   float Mrow[NV];
   Dof d;
-  forward<NV, true>(m, s, lane, Mrow, d);   // efc_D kept out of noslip's parking
+  forward<TASK, true>(m, s, lane, Mrow, d);   // efc_D kept out of noslip's parking
   for (int i = lane; i < MAXB * 3; i += 64) out[i] = i < m.nbody * 3 ? (&s.xpos[0][0])[i] : 0.f;
   for (int i = lane; i < MAXB * 4; i += 64) out[96 + i] = i < m.nbody * 4 ? (&s.xquat[0][0])[i] : 0.f;
   for (int i = lane; i < MAXS * 3; i += 64) out[224 + i] = i < m.nsite * 3 ? (&s.sxpos[0][0])[i] : 0.f;
@@ -619,8 +628,9 @@ __global__ void __launch_bounds__(64) k_collide_test(DModel m, int n, const int*
 struct CamRec {
   float c[AW_CAM_FLOATS];
 };
-template <int NV>
+template <int TASK>
 __global__ void __launch_bounds__(256) k_depth(DModel m, DState st, int n, CamRec cam, int W, int H, float* out) {
+  constexpr int NV = Tree<TASK>::NV;
   __shared__ Env s;
   __shared__ RGeoms rg;
   const int env = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
@@ -1019,57 +1029,82 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
 }
 
 // resident k_step workgroups on the handle's device (occupancy x CUs): the persistent grid
-template <int NV>
+template <int TASK>
 static int step_slots(int device) {
   int per_cu = 0, cus = 0;
-  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_step<NV>, 64, 0);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_step<TASK>, 64, 0);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
   return std::max(per_cu, 1) * std::max(cus, 1);
 }
-template <int NV>
+template <int TASK>
 static void launch_step(aw_handle* h, const float* a, float* obs, float* rew, uint8_t* done, uint8_t* goal,
                         float* tobs, int autoreset, uint64_t seed, hipStream_t st) {
   // grid = the handle's persistent slot count (aw_create / aw_set_option), capped at nenv
   const int grid = std::min(h->nenv, h->slots);
   if (grid < h->nenv) (void)hipMemsetAsync(h->next_env, 0, sizeof(int), st);
-  hipLaunchKernelGGL((k_step<NV>), dim3(grid), dim3(64), 0, st, h->m, (const DModel*)h->dmhdr, h->st, h->nenv, a, obs, rew, done,
+  hipLaunchKernelGGL((k_step<TASK>), dim3(grid), dim3(64), 0, st, h->m, (const DModel*)h->dmhdr, h->st, h->nenv, a, obs, rew, done,
                      goal, tobs, autoreset, seed, h->next_env);
 }
-template <int NV>
+template <int TASK>
 static void launch_reset(aw_handle* h, const uint8_t* mask, const float* params, uint64_t seed, float* obs,
                          hipStream_t st) {
-  hipLaunchKernelGGL((k_reset<NV>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, mask, params, seed, obs);
+  hipLaunchKernelGGL((k_reset<TASK>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, mask, params, seed, obs);
 }
-template <int NV>
+template <int TASK>
 static void launch_set(aw_handle* h, const float* q, const float* v, const float* w, const float* p, float* obs,
                        hipStream_t st) {
-  hipLaunchKernelGGL((k_set_state<NV>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, q, v, w, p, obs);
+  hipLaunchKernelGGL((k_set_state<TASK>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, q, v, w, p, obs);
 }
-template <int NV>
+template <int TASK>
 static void launch_dump(aw_handle* h, int env, const float* ctrl, float* out, hipStream_t st) {
-  hipLaunchKernelGGL((k_dump<NV>), dim3(1), dim3(64), 0, st, h->m, h->st, env, ctrl, out);
+  hipLaunchKernelGGL((k_dump<TASK>), dim3(1), dim3(64), 0, st, h->m, h->st, env, ctrl, out);
 }
 
-template <int NV>
+template <int TASK>
 static void launch_depth(aw_handle* h, const CamRec& cam, int W, int H, float* out, hipStream_t st) {
-  hipLaunchKernelGGL((k_depth<NV>), dim3(h->nenv), dim3(256), 0, st, h->m, h->st, h->nenv, cam, W, H, out);
+  hipLaunchKernelGGL((k_depth<TASK>), dim3(h->nenv), dim3(256), 0, st, h->m, h->st, h->nenv, cam, W, H, out);
 }
 
-#ifdef AW_ONLY_NV
-#define DISPATCH_NV(NVV, CALL)                                                     \
-  switch (NVV) {                                                                   \
-    case AW_ONLY_NV: CALL(AW_ONLY_NV); break;                                      \
-    default: return fail(AW_EUNSUPPORTED, "nv not instantiated in this build");   \
+// kernels are instantiated per task (the dof tree of aw_trees.h is a template argument)
+#ifdef AW_ONLY_TASK
+#define DISPATCH_TASK(T, CALL)                                                     \
+  switch (T) {                                                                     \
+    case AW_ONLY_TASK: CALL(AW_ONLY_TASK); break;                                  \
+    default: return fail(AW_EUNSUPPORTED, "task not instantiated in this build");  \
   }
 #else
-#define DISPATCH_NV(NVV, CALL)                                                     \
-  switch (NVV) {                                                                   \
-    case 30: CALL(30); break;                                                      \
-    case 33: CALL(33); break;                                                      \
-    case 36: CALL(36); break;                                                      \
-    default: return fail(AW_EUNSUPPORTED, "nv not instantiated (30/33/36)");      \
+#define DISPATCH_TASK(T, CALL)                                                     \
+  switch (T) {                                                                     \
+    case 0: CALL(0); break;                                                        \
+    case 1: CALL(1); break;                                                        \
+    case 2: CALL(2); break;                                                        \
+    case 3: CALL(3); break;                                                        \
+    default: return fail(AW_EUNSUPPORTED, "task kind not instantiated (0..3)");   \
   }
 #endif
+
+// the model's dof tree must be the compiled one of its task (aw_trees.h, tools/gen_trees.py)
+template <int TASK>
+static bool tree_matches(const std::vector<int>& par) {
+  if ((int)par.size() != TreeDef<TASK>::NV) return false;
+  for (int j = 0; j < TreeDef<TASK>::NV; j++)
+    if (par[j] != TreeDef<TASK>::parent[j]) return false;
+  return true;
+}
+static int check_tree(const Blob& B, int task_kind) {
+  const std::vector<int> par = B.i("dof_parentid");
+  bool ok = false;
+  switch (task_kind) {
+    case 0: ok = tree_matches<0>(par); break;
+    case 1: ok = tree_matches<1>(par); break;
+    case 2: ok = tree_matches<2>(par); break;
+    case 3: ok = tree_matches<3>(par); break;
+    default: return fail(AW_EUNSUPPORTED, "unknown task kind");
+  }
+  if (!ok) return fail(AW_EUNSUPPORTED, "model dof tree differs from the compiled tree of its task "
+                                        "(mj_envs_amd/csrc/aw_trees.h: run tools/gen_trees.py and rebuild)");
+  return AW_OK;
+}
 
 // persistent grid of the k_step instantiation the handle currently selects
 static int update_slots(aw_handle* h) {
@@ -1077,8 +1112,8 @@ static int update_slots(aw_handle* h) {
     h->slots = h->grid_env > 0 ? h->grid_env : (1 << 30);
     return AW_OK;
   }
-#define CALL(NVV) (h->slots = step_slots<NVV>(h->device))
-  DISPATCH_NV(h->NV, CALL)
+#define CALL(TT) (h->slots = step_slots<TT>(h->device))
+  DISPATCH_TASK(h->m.task_kind, CALL)
 #undef CALL
   return AW_OK;
 }
@@ -1093,7 +1128,6 @@ static void free_handle(aw_handle* h) {
   if (h->dmhdr) (void)hipFree(h->dmhdr);
   if (h->dstate) (void)hipFree(h->dstate);
   if (h->m.jspill) (void)hipFree(h->m.jspill);
-  if (h->m.msave) (void)hipFree(h->m.msave);
   if (h->next_env) (void)hipFree(h->next_env);
   delete h;
 }
@@ -1122,13 +1156,12 @@ int aw_create(const void* blob, size_t nbytes, int n_envs, int device, aw_handle
   std::unique_ptr<MData> md(new MData());   // value-initialised: zero
   if (int rc = build_model(B, h->m, *md)) return rc;
   h->NV = h->m.nv;
-  if (h->NV != 30 && h->NV != 33 && h->NV != 36) return fail(AW_EUNSUPPORTED, "nv not instantiated");
+  if (int rc = check_tree(B, h->m.task_kind)) return rc;
   HIPCHK(hipSetDevice(device));
   HIPCHK(hipMalloc(&h->dmodel, sizeof(MData)));
   HIPCHK(hipMemcpy(h->dmodel, md.get(), sizeof(MData), hipMemcpyHostToDevice));
   h->m.d = (const MData*)h->dmodel;
   HIPCHK(hipMalloc((void**)&h->m.jspill, (size_t)n_envs * JSPILL * sizeof(float)));
-  HIPCHK(hipMalloc((void**)&h->m.msave, (size_t)n_envs * NPACK_SAVE * sizeof(float)));
   HIPCHK(hipMalloc(&h->dmhdr, sizeof(DModel) + sizeof(DState)));
   HIPCHK(hipMalloc((void**)&h->next_env, sizeof(int)));
   const size_t bytes = layout_state(h.get(), nullptr);   // dry run: sizes only
@@ -1180,8 +1213,8 @@ int aw_set_option(aw_handle* h, int disableflags, int iterations, int noslip_ite
 int aw_reset(aw_handle* h, const uint8_t* mask, const float* params, uint64_t seed, float* obs, void* stream) {
   if (!h) return fail(AW_EINVAL, "aw_reset: null");
   HIPCHK(hipSetDevice(h->device));
-#define CALL(NVV) launch_reset<NVV>(h, mask, params, seed, obs, (hipStream_t)stream)
-  DISPATCH_NV(h->NV, CALL)
+#define CALL(TT) launch_reset<TT>(h, mask, params, seed, obs, (hipStream_t)stream)
+  DISPATCH_TASK(h->m.task_kind, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());
   return AW_OK;
@@ -1191,8 +1224,8 @@ int aw_step(aw_handle* h, const float* actions, float* obs, float* reward, uint8
             float* terminal_obs, int autoreset, uint64_t seed, void* stream) {
   if (!h || !actions || !obs || !reward || !done || !goal) return fail(AW_EINVAL, "aw_step: null buffer");
   HIPCHK(hipSetDevice(h->device));
-#define CALL(NVV) launch_step<NVV>(h, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, (hipStream_t)stream)
-  DISPATCH_NV(h->NV, CALL)
+#define CALL(TT) launch_step<TT>(h, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, (hipStream_t)stream)
+  DISPATCH_TASK(h->m.task_kind, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());
   return AW_OK;
@@ -1225,8 +1258,8 @@ int aw_set_state(aw_handle* h, const float* qpos, const float* qvel, const float
                  float* obs, void* stream) {
   if (!h) return fail(AW_EINVAL, "aw_set_state: null");
   HIPCHK(hipSetDevice(h->device));
-#define CALL(NVV) launch_set<NVV>(h, qpos, qvel, warm, params, obs, (hipStream_t)stream)
-  DISPATCH_NV(h->NV, CALL)
+#define CALL(TT) launch_set<TT>(h, qpos, qvel, warm, params, obs, (hipStream_t)stream)
+  DISPATCH_TASK(h->m.task_kind, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());
   return AW_OK;
@@ -1332,8 +1365,8 @@ int aw_task_eval(aw_handle* h, int n, const float* qpos, const float* qvel, cons
 int aw_forward_dump(aw_handle* h, int env, const float* ctrl, float* out, void* stream) {
   if (!h || !out || env < 0 || env >= h->nenv) return fail(AW_EINVAL, "aw_forward_dump: bad arguments");
   HIPCHK(hipSetDevice(h->device));
-#define CALL(NVV) launch_dump<NVV>(h, env, ctrl, out, (hipStream_t)stream)
-  DISPATCH_NV(h->NV, CALL)
+#define CALL(TT) launch_dump<TT>(h, env, ctrl, out, (hipStream_t)stream)
+  DISPATCH_TASK(h->m.task_kind, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());
   return AW_OK;
@@ -1345,8 +1378,8 @@ int aw_render_depth(aw_handle* h, const float* cam, int width, int height, float
   HIPCHK(hipSetDevice(h->device));
   CamRec c;
   memcpy(c.c, cam, sizeof(c.c));   // host array: the camera record travels as a kernel argument
-#define CALL(NVV) launch_depth<NVV>(h, c, width, height, out, (hipStream_t)stream)
-  DISPATCH_NV(h->NV, CALL)
+#define CALL(TT) launch_depth<TT>(h, c, width, height, out, (hipStream_t)stream)
+  DISPATCH_TASK(h->m.task_kind, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());
   return AW_OK;

@@ -204,7 +204,6 @@ struct DModel {
   int nrgeom;                 // rendered geoms
   const MData* __restrict__ d;
   float* jspill;              // per-env dense-J overflow rows [nenv][JSPILL] (device)
-  float* msave;               // per-env copy of the smooth solve's factor of M [nenv][NPACK_SAVE]
   unsigned long long env_offset;   // global id of env 0 of this handle (shards): Philox keys
 };
 
@@ -223,7 +222,6 @@ struct DModel {
 // 16-byte aligned tri(j), so uniform reads along a row are ds_read_b128 broadcasts
 __host__ __device__ constexpr int tri(int j) { return 4 * (j + 2 * (j / 4) * (j / 4 - 1) + (j % 4) * (j / 4)); }
 constexpr int NPACK = tri(MAXV);
-constexpr int NPACK_SAVE = ((NPACK + 255) / 256) * 256;   // 64 lanes x 16-byte chunks
 
 struct __attribute__((aligned(16))) Env {
   union {
@@ -289,6 +287,18 @@ AW_DEV float rlane(float x, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
 }
 AW_DEV int rlane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+// An opaque copy of a lane-dependent value: values derived from it cannot be hoisted above this
+// point (out of the substep loop) to sit in registers across every stage.
+AW_DEV int opaque(int x) {
+  int y;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+  return y;
+}
+AW_DEV float opaque(float x) {
+  float y;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+  return y;
+}
 // Intra-wave LDS hand-off.  Every workgroup is exactly one wave64: LDS operations of a wave
 // execute in issue order, so cross-lane communication through LDS needs only a compiler-level
 // ordering point, not s_barrier + a full s_waitcnt drain (which would serialise every

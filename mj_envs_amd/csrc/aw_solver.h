@@ -13,6 +13,7 @@
 //     instead of a dual residual matrix.
 #pragma once
 #include "aw_common.h"
+#include "aw_tree.h"
 
 namespace aw {
 
@@ -22,6 +23,9 @@ namespace aw {
 // pulls the column back with 16-byte broadcast reads for its rank-1 update.  Entries above a
 // lane's diagonal (and rows of lanes >= NV) take unmasked garbage updates that are never read:
 // the factor proper is the lower triangle of lanes < NV.
+#ifndef AW_CHOL_LA
+#define AW_CHOL_LA 2
+#endif
 #ifdef AW_CHOL_READLANE
 // Variant: the column is broadcast with v_readlane (SGPR operands) instead of an LDS round trip.
 template <int NV>
@@ -38,11 +42,12 @@ AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
     for (int k = j + 1; k < NV; k++) row[k] = fmaf(-lij, rlane(lij, k), row[k]);
   }
 }
-#elif defined(AW_CHOL_LA)
-// Look-ahead: column j's entries for the next AW_CHOL_LA pivot rows (j+1 .. j+LA) travel by
-// v_readlane (SGPR broadcast) and update those rows at once, so pivot j+1 waits only on this
-// column's readlane, not on the LDS round trip; the rest of the rank-1 update (rows > j+LA) reads
-// the column from LDS as before and lags behind the pivot chain.
+#elif AW_CHOL_LA > 0
+// Look-ahead (default; -DAW_CHOL_LA=0 selects the plain form below): column j's entries for the
+// next AW_CHOL_LA pivot rows (j+1 .. j+LA) travel by v_readlane (SGPR broadcast) and update those
+// rows at once, so pivot j+1 waits only on this column's readlane, not on the LDS round trip; the
+// rest of the rank-1 update (rows > j+LA) reads the column from LDS and lags behind the pivot
+// chain.  Same operands in every fma: bitwise the plain form's factor (A/B -0.35 %, r03d).
 template <int NV>
 AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
   constexpr int LA = AW_CHOL_LA;
@@ -169,29 +174,6 @@ AW_DEV void jput(const DModel& m, Env& s, int d, int k, float v) {
 AW_DEV void jspill_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-// The smooth solve's factor of M is needed again by noslip (inv(M)) after Newton has reused the
-// LDS factor storage: it is parked in this env's global block (L2-resident, 16-byte vector
-// stores / loads, lane-dependent addresses) instead of refactoring M.
-typedef float f4v __attribute__((ext_vector_type(4)));
-AW_DEV gp_t<f4v> msave_block(const DModel& m, const Env& s) {
-  return (gp_t<f4v>)(gmp(m.msave) + (size_t)s.slot * NPACK_SAVE);
-}
-template <int NV>
-AW_DEV void msave_store(const DModel& m, const Env& s, int lane) {
-  constexpr int n4 = (tri(NV) + 3) / 4;
-  gp_t<f4v> dst = msave_block(m, s);
-  const f4v* src = reinterpret_cast<const f4v*>(s.L);
-  for (int i = lane; i < n4; i += 64) dst[i] = src[i];
-}
-template <int NV>
-AW_DEV void msave_load(const DModel& m, Env& s, int lane) {
-  constexpr int n4 = (tri(NV) + 3) / 4;
-  jspill_fence();   // the stores of msave_store (same wave) are complete
-  gp_t<const f4v> src = msave_block(m, s);
-  f4v* dst = reinterpret_cast<f4v*>(s.L);
-  for (int i = lane; i < n4; i += 64) dst[i] = src[i];
 }
 
 // J_r . x  (x in LDS); r is per lane
@@ -859,47 +841,20 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
 
 // ---------------------------------------------------------------------------------------
 // noslip: PGS over frictionloss rows and opposing pyramid-edge pairs, no regularisation
-template <int NV, bool KEEP_D>
-AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[NV], float& qacc) {
+template <int TASK, bool KEEP_D>
+AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[Tree<TASK>::NV], float& qacc) {
+  constexpr int NV = Tree<TASK>::NV;
   const int nsparse = s.nsparse, ndense = s.ndense;
-  // inv(M): factor, then lane i solves M x = e_i (multi-RHS, L entries broadcast from LDS);
-  // lane i keeps row i of inv(M) in VGPRs (symmetric: row == column)
+  // inv(M) from the tree factor of M (aw_tree.h): lane i keeps row i of inv(M) in VGPRs
+  // (symmetric: row == column)
   float Mi[NV];
   {
     float row[NV];
-#ifdef AW_NOSLIP_REFACTOR
 #pragma unroll
     for (int k = 0; k < NV; k++) row[k] = Mrow[k];
-    float invd = 1.f;
-    chol_factor<NV>(row, lane, invd, s);
-    chol_store<NV>(row, lane, s);
-    if (lane < NV) s.vec2[lane] = invd;
-#else
-    (void)row;
-    msave_load<NV>(m, s, lane);
-    wsync();
-    if (lane < NV) s.vec2[lane] = __builtin_amdgcn_rcpf(s.L[tri(lane) + lane]);
-#endif
-    wsync();
-  }
-#pragma unroll
-  for (int j = 0; j < NV; j++) {
-    float acc = (j == lane) ? 1.f : 0.f;
-#pragma unroll
-    for (int k = 0; k < j; k++) acc = fmaf(-s.L[tri(j) + k], Mi[k], acc);
-    Mi[j] = acc * s.vec2[j];
-    __builtin_amdgcn_sched_barrier(0);
-  }
-#pragma unroll
-  // backward, right-looking: finish entry j, then eliminate it from entries k < j with row j
-  // of L (a contiguous, 16-byte aligned row: broadcast b128 reads; the left-looking form read
-  // the factor by columns, one b32 per entry)
-  for (int j = NV - 1; j >= 0; j--) {
-    Mi[j] *= s.vec2[j];
-    const float mj = Mi[j];
-#pragma unroll
-    for (int k = 0; k < j; k++) Mi[k] = fmaf(-s.L[tri(j) + k], mj, Mi[k]);
-    __builtin_amdgcn_sched_barrier(0);
+    float invd;
+    tree_factor<TASK>(row, invd, lane);
+    tree_inverse<TASK>(row, invd, lane, Mi);
   }
   if (lane >= NV) {
 #pragma unroll
@@ -952,9 +907,6 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
   // are parked in dead LDS, the rest are rebuilt each sweep.
   int npr = 0, pr_e = 0;
   float pr_k = 0.f, pr_ik = 0.f, pr_ard = 0.f;
-#ifdef AW_NS_BLOCK
-  float pc1 = 0.f, pc2 = 0.f, pc3 = 0.f;   // lane p: jd_p . xd_p-1, xd_p-2, xd_p-3 within p's block
-#endif
   float c_jd[NSP_CACHE], c_xd[NSP_CACHE];
 #pragma unroll
   for (int p = 0; p < NSP_CACHE; p++) c_jd[p] = c_xd[p] = 0.f;
@@ -988,22 +940,6 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
       pr_e = e; pr_k = K; pr_ik = 1.0f / K;
       pr_ard = s.efc_aref[nsparse + e] - s.efc_aref[nsparse + e + 1];
     }
-#ifdef AW_NS_BLOCK
-    // couplings jd_p . xd_p-k to the earlier pairs of p's block of 4 (blocked Gauss-Seidel below)
-    if (p < NSP_CACHE && (p & 3)) {
-      float x1 = 0.f, x2 = 0.f, x3 = 0.f;
-#pragma unroll
-      for (int q = 0; q < NSP_CACHE; q++) {
-        x1 = q == p - 1 ? c_xd[q] : x1;
-        x2 = q == p - 2 ? c_xd[q] : x2;
-        x3 = q == p - 3 ? c_xd[q] : x3;
-      }
-      const float k1 = wave_sum(jd * x1);
-      const float k2 = (p & 3) >= 2 ? wave_sum(jd * x2) : 0.f;
-      const float k3 = (p & 3) >= 3 ? wave_sum(jd * x3) : 0.f;
-      if (lane == p) { pc1 = k1; pc2 = k2; pc3 = k3; }
-    }
-#endif
 #pragma unroll
     for (int q = 0; q < NSP_CACHE; q++)
       if (q == p) { c_jd[q] = jd; c_xd[q] = xd; }
@@ -1079,48 +1015,9 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
         if (lane + 64 == e + 1) fd_hi = f2n;
       }
     };
-#ifdef AW_NS_BLOCK
-    // Blocked Gauss-Seidel over the cached pairs, four at a time: the four residual sums
-    // jd_p . qacc are taken at once against the block's starting qacc (independent reductions
-    // that overlap), and pair p's sum is then corrected by the couplings jd_p . xd_q to the
-    // block's earlier pairs q times their updates d_q -- the same sweep as one pair at a time
-    // (r_p = jd_p . (qacc + sum_q xd_q d_q)), with one reduction latency per block on the chain.
-    auto pair_upd = [&](int p, float sq) {
-      const int e = rlane_i(pr_e, p);
-      const float f1 = fd_get(e), f2 = fd_get(e + 1);
-      const float ik = rlane(pr_ik, p), ard = rlane(pr_ard, p);
-      const float d1 = __builtin_amdgcn_fmed3f(fmaf(-sq, ik, ard * ik), -f1, f2);
-      const float rd = sq - ard;
-      const float f1n = f1 + d1, f2n = f2 - d1;
-      impr -= rd * d1 + 0.5f * rlane(pr_k, p) * d1 * d1;
-      if (e < 64) {
-        if (lane == e) fd = f1n;
-        if (lane == e + 1) fd = f2n;
-        if (e == 63 && lane == 0) fd_hi = f2n;
-      } else {
-        if (lane + 64 == e) fd_hi = f1n;
-        if (lane + 64 == e + 1) fd_hi = f2n;
-      }
-      return d1;
-    };
-#pragma unroll
-    for (int b = 0; b < NSP_CACHE; b += 4) {
-      if (b < npr) {
-        const float s0 = wave_sum(c_jd[b] * qacc), s1 = wave_sum(c_jd[b + 1] * qacc);
-        const float s2 = wave_sum(c_jd[b + 2] * qacc), s3 = wave_sum(c_jd[b + 3] * qacc);
-        const float d0 = pair_upd(b, s0);
-        const float d1 = pair_upd(b + 1, fmaf(rlane(pc1, b + 1), d0, s1));
-        const float d2 = pair_upd(b + 2, fmaf(rlane(pc1, b + 2), d1, fmaf(rlane(pc2, b + 2), d0, s2)));
-        const float d3 = pair_upd(b + 3, fmaf(rlane(pc1, b + 3), d2, fmaf(rlane(pc2, b + 3), d1,
-                                                                       fmaf(rlane(pc3, b + 3), d0, s3))));
-        qacc = fmaf(c_xd[b], d0, fmaf(c_xd[b + 1], d1, fmaf(c_xd[b + 2], d2, fmaf(c_xd[b + 3], d3, qacc))));
-      }
-    }
-#else
 #pragma unroll
     for (int p = 0; p < NSP_CACHE; p++)
       if (p < npr) pair_step(p, c_jd[p], c_xd[p]);
-#endif
     for (int p = NSP_CACHE; p < npr; p++) {
       float jd, xd;
 #ifndef AW_NOSLIP_NOLDS

@@ -6,8 +6,8 @@ Tolerances (stated per the north star's "fp32 tolerance"):
   * forward internals from identical states: relative (max-norm) error <= 1e-4 for kinematics,
     M, qacc_smooth; qacc / constraint force <= 2e-3 (Newton on the soft problem in fp32).
   * one env-step (frame_skip mj_steps) from identical states: qpos |err| <= 2e-5 + 1e-5|q|,
-    qvel |err| <= 5e-3 (1 + |v|) in >= 95% of envs; the rest may differ only where a contact
-    switches on/off at the margin in one precision and not the other (discrete event).
+    qvel |err| <= 5e-3 (1 + |v|) in >= 99.5 % of envs / (env, step) cases; the rest may differ
+    only where a contact switches on/off at the margin in one precision and not the other.
 """
 import numpy as np
 import pytest
@@ -89,8 +89,9 @@ def rel(a, b):
 # remainder are discrete events: a contact within fp32 rounding of the margin, or a bonus
 # threshold, switching in one precision and not the other.
 ONE_STEP_MIN = 0.995
-VARIATION_MIN = 0.9     # 'pos' (measured 0.94): the hammer rests on its moved cylinder head; every
-                        # miss must be a discrete event (_discrete_event)
+VARIATION_MIN = 0.995   # 'pos' measured 0.94 in round 2 (the hammer rests on its moved cylinder
+                        # head: the MPR line contact), 1.0 with MPR on fp64 geometry; every miss
+                        # must still be a discrete event (_discrete_event)
 REWARD_MIN = 0.995
 
 # Grasp regime (DAPG policies; hammer: fingers closed on the handle, head striking the nail):
@@ -171,6 +172,43 @@ def test_forward_internals_match_oracle(env_id):
             assert d["nefc"] == int(sc[1])
             assert rel(d["qacc"], o.get("qacc")) < 2e-3, (env_id, e)
     assert ncon_total > 0 or env_id == "door-v0"
+
+
+def test_forward_dump_rows_in_grasp_regime():
+    """aw_forward_dump's constraint rows (efc_D, aref, type) on DAPG grasp states with the most
+    dense rows: noslip parks its pair rows in dead LDS, and the dump kernel keeps efc_D out of
+    that parking, so the reported rows are the solver's (tools/diag_tf.py compares them)."""
+    import os
+    from conftest import GOLDEN
+    from mj_envs_amd.policy import GaussianMLP
+    env_id, n = "hammer-v0", 64
+    m, o = make_oracle(env_id)
+    _, sim = _sim(env_id, n)
+    pol = GaussianMLP.from_npz(os.path.join(GOLDEN, "dapg_hammer.npz"))
+    obs = sim.empty(n, sim.obs_dim)
+    sim.reset(obs, seed=21)
+    rew, done, goal = sim.empty(n), sim.empty(n, dtype=torch.uint8), sim.empty(n, dtype=torch.uint8)
+    for _ in range(120):
+        sim.step(_t(pol.mean_np(obs.cpu().numpy())), obs, rew, done, goal)
+    q, v, w, p = sim.empty(n, sim.nq), sim.empty(n, sim.nv), sim.empty(n, sim.nv), sim.empty(n, sim.nparam)
+    sim.get_state(q, v, w, p)
+    torch.cuda.synchronize()
+    dumps = [sim.forward_dump(e) for e in range(n)]
+    order = np.argsort([-d["ndense"] for d in dumps])[:8]
+    assert dumps[order[0]]["ndense"] > 40, dumps[order[0]]["ndense"]
+    checked = 0
+    for e in order:
+        d = dumps[e]
+        o.forward1(p[e].cpu().numpy().astype(np.float64), q[e].cpu().numpy().astype(np.float64),
+                   v[e].cpu().numpy().astype(np.float64), w[e].cpu().numpy().astype(np.float64))
+        if d["nefc"] != int(o.get("scalars")[1]):
+            continue                          # a contact decided by fp32 rounding: rows differ
+        np.testing.assert_array_equal(d["efc_type"], o.get("efc_type"))
+        np.testing.assert_allclose(d["efc_D"], o.get("efc_D"), rtol=2e-3)
+        np.testing.assert_allclose(d["efc_aref"], o.get("efc_aref"), rtol=2e-3, atol=2e-3)
+        checked += 1
+    print(f"forward_dump rows: {checked} grasp states, max dense rows {dumps[order[0]]['ndense']}")
+    assert checked >= 4
 
 
 @pytest.mark.parametrize("env_id", ENVS)
@@ -316,22 +354,31 @@ def test_determinism():
     assert torch.equal(outs[0], outs[1])
 
 
-# Minimum fraction of (env, step) cases within the one-step tolerance.  pen-v0 is lower: while
-# the pen falls onto the fingers |qacc| reaches ~1e3, the fp32 Newton solution carries ~1e-3
-# absolute error into the residuals of the (unconverged, tolerance 1e-6) noslip PGS, whose early
-# exit then lands one sweep apart from the fp64 oracle's (6 vs 5 sweeps: ~1 % qacc change in that
-# substep).  tools/debug_sub.py shows forward internals identical to 4e-7 relative up to that
-# substep.
+# Minimum fraction of (env, step) cases within the one-step tolerance, for every task and regime
+# (random actions, DAPG grasping, C3 at full size, the 4 096-env headline configuration).  The
+# remainder are discrete events: a contact or row within fp32 rounding of its activation margin.
 TEACHER_FORCED_MIN = {"hammer-v0": 0.995, "door-v0": 0.995, "relocate-v0": 0.995, "pen-v0": 0.995}
-GRASP_MIN = {"hammer-v0": 0.995, "door-v0": 0.995, "pen-v0": 0.99, "relocate-v0": 0.995}
-# C3 at full size: hammer-v0 measured 0.9947 (273 of 51 200).  The misses are one replicated
-# configuration: at step 28 the untouched hammer has settled identically in most of the 256 envs
-# (resets randomise only the board), and tools/diag_tf.py (profiles/r02n_diag_c3_hammer.json)
-# finds 15 of the 16 misses it lists at that step with identical dqpos (4.402e-5) in every env,
-# attributed to the last substep: same ncon / nefc, contact normals equal to 1e-6, one contact
-# point 2.3 cm apart -- a degenerate (line / face) contact whose point is ill-conditioned in the
-# last bits of its inputs, as MPR's is on a cylinder lying flat.
-C3_MIN = {"hammer-v0": 0.99, "door-v0": 0.995, "pen-v0": 0.995, "relocate-v0": 0.995}
+GRASP_MIN = {"hammer-v0": 0.995, "door-v0": 0.995, "pen-v0": 0.995, "relocate-v0": 0.995}
+# C3 at full size.  Round 2 measured hammer-v0 at 0.9939: tools/diag_tf.py attributed 38 of 40
+# misses (profiles/r03a_diag_c3_hammer.json) to one contact -- the hammer's cylinder head lying
+# on the table, a line contact whose MPR point jumps between the ends of the line under 1e-7 rad
+# of rotation (fp32 kinematics) while the fp64 oracle is stable under input rounding.  MPR now
+# runs on fp64 geometry (aw_dynamics.h stage_kin64): 0.9999 (r03d, 7 of 51 200).
+C3_MIN = {"hammer-v0": 0.995, "door-v0": 0.995, "pen-v0": 0.995, "relocate-v0": 0.995}
+
+
+@pytest.mark.parametrize("env_id", ENVS)
+def test_teacher_forced_trajectory(env_id):
+    frac = _teacher_forced(env_id, 0)
+    assert frac >= TEACHER_FORCED_MIN[env_id], (env_id, frac)
+
+
+@pytest.mark.parametrize("env_id", ENVS)
+def test_teacher_forced_dapg_grasp(env_id):
+    """Teacher forcing along DAPG-policy rollouts (grasp / manipulation regime: up to ~20
+    contacts and ~100 dense rows per substep), oracle at MuJoCo's capacities, no overflow."""
+    frac = _teacher_forced(env_id, 0, policy=True, steps=80)
+    assert frac >= GRASP_MIN[env_id], (env_id, frac)
 
 
 @pytest.mark.parametrize("env_id", ENVS)

@@ -61,8 +61,10 @@ def test_checker_analytic():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env_id", ["hammer-v0", "door-v0"])
+@pytest.mark.parametrize("env_id", ENVS)
 def test_gpu_depth_vs_checker(env_id):
+    """BASELINE config 5's depth path on every task: 16 envs after 6 random steps (pen's camera
+    elevation comes from its 'target' body, pen_v0.py:163-177; door / relocate from body 0)."""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -71,7 +73,7 @@ def test_gpu_depth_vs_checker(env_id):
     from mj_envs_amd.tasks import attach_task, load_model
     from oracle.depth import oracle_geoms, render_depth
     m, orc = make_oracle(env_id)
-    n, W, H = 4, 64, 64
+    n, W, H = 16, 64, 64
     sim = _native.Sim(m.to_blob(), n)
     obs = sim.empty(n, sim.obs_dim)
     sim.reset(obs, seed=3)

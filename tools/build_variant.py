@@ -13,5 +13,5 @@ from __graft_entry__ import HIPCC_FLAGS, HIP_SRC  # noqa: E402
 
 name, flags = sys.argv[1], sys.argv[2:]
 out = os.path.join(REPO, "mj_envs_amd", f"libadroit_hip_{name}.so")
-subprocess.run(["/opt/rocm/bin/hipcc", *HIPCC_FLAGS, "-DAW_ONLY_NV=33", *flags, "-o", out, HIP_SRC], check=True)
+subprocess.run(["/opt/rocm/bin/hipcc", *HIPCC_FLAGS, "-DAW_ONLY_TASK=0", *flags, "-o", out, HIP_SRC], check=True)
 print(out)

@@ -12,8 +12,8 @@ echo "[gpu] diag"
 timeout -k 10 600 python -u tools/diag_tf.py hammer-v0 random 200 256 20 > $OUT/diag.log 2>&1
 cp gpurun_out/diag_hammer_random.json $OUT/
 echo "[gpu] ab"
-bash tools/ab.sh main flat ftz la1 la2 ftzla2 nsb > $OUT/ab_random.txt 2>&1
+bash tools/ab.sh main base tftz tla2 tnsb ftz flat > $OUT/ab_random.txt 2>&1
 cat $OUT/ab_random.txt
-bash tools/ab.sh -p dapg main nsb ftzla2 > $OUT/ab_dapg.txt 2>&1
+bash tools/ab.sh -p dapg main base tnsb > $OUT/ab_dapg.txt 2>&1
 cat $OUT/ab_dapg.txt
 echo "[gpu] done"

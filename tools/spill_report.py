@@ -1,15 +1,15 @@
-"""Attribute scratch (spill) instructions of k_step<NV> to source lines (debug .s build)."""
+"""Attribute scratch (spill) instructions of k_step<TASK> to source lines (debug .s build)."""
 import collections, re, subprocess, sys
-nv = sys.argv[1] if len(sys.argv) > 1 else "33"
+task = sys.argv[1] if len(sys.argv) > 1 else "0"   # task kind (hammer 0)
 src = "mj_envs_amd/csrc/adroit_wave.hip"
 subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-g", "-S", "--cuda-device-only",
-                f"-DAW_ONLY_NV={nv}", "-o", "/tmp/isa/one.s", src], check=True)
+                f"-DAW_ONLY_TASK={task}", "-o", "/tmp/isa/one.s", src], check=True)
 lines = open("/tmp/isa/one.s").readlines()
 fmap = {}
 for l in lines:
     m = re.match(r'\s*\.file\s+(\d+)\s+"[^"]*"\s+"([^"]+)"', l)
     if m: fmap[m.group(1)] = m.group(2)
-s = next(i for i, l in enumerate(lines) if l.startswith(f"_Z6k_stepILi{nv}"))
+s = next(i for i, l in enumerate(lines) if l.startswith(f"_Z6k_stepILi{task}"))
 e = next(i for i in range(s + 1, len(lines)) if lines[i].startswith(".Lfunc_end"))
 cur = None; cnt = collections.Counter(); n = 0
 for l in lines[s:e]:

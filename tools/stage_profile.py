@@ -16,10 +16,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF_LIB = os.path.join(REPO, "mj_envs_amd", "libadroit_hip_prof.so")
 
 
-def build(nv: int = 33):
+def build(task: int = 0):
     sys.path.insert(0, REPO)
     from __graft_entry__ import HIPCC_FLAGS
-    cmd = ["/opt/rocm/bin/hipcc", *HIPCC_FLAGS, "-DAW_STAGE_PROF", f"-DAW_ONLY_NV={nv}", "-o", PROF_LIB,
+    cmd = ["/opt/rocm/bin/hipcc", *HIPCC_FLAGS, "-DAW_STAGE_PROF", f"-DAW_ONLY_TASK={task}", "-o", PROF_LIB,
            os.path.join(REPO, "mj_envs_amd", "csrc", "adroit_wave.hip")]
     subprocess.run(cmd, check=True)
 
@@ -37,7 +37,9 @@ def main():
                          "(mean action, grasp regime)")
     a = ap.parse_args()
     if a.build:
-        build()
+        sys.path.insert(0, REPO)
+        from mj_envs_amd.tasks import TASKS
+        build(TASKS[a.env].kind)
         return
     os.environ["AW_LIB"] = PROF_LIB
     sys.path.insert(0, REPO)
