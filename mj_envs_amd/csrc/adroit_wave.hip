@@ -133,6 +133,13 @@ AW_DEV void stage_collision(const DModel& m, Env& s, int lane) {
     narrow_class<3>(m, s, plist, cnt[3], lane);
     AW_PROF(s, PR_CO_C3);
     if (cnt[4] > 0) {
+      // the surviving MPR pairs' body closures: only those frames are computed in fp64
+      if (lane == 0) s.kin64_mask = 0ull;
+      wsync();
+      unsigned long long km = 0ull;
+      for (int i = lane; i < cnt[4]; i += 64) km |= MD(cp_kin64, plist[m.cls_start[4] + i]);
+      if (km) atomicOr(&s.kin64_mask, km);
+      wsync();
       stage_kin64(m, s, lane);
       AW_PROF(s, PR_CO_KIN64);
       narrow_class<4>(m, s, plist, cnt[4], lane);
@@ -342,7 +349,9 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
   const DModel& m = mval;
   (void)mptr;
 #endif
-#ifdef AW_STATE_PTR
+#ifndef AW_STATE_BYVAL
+  // the state pointers read from the device header where they are used (the loop's memory
+  // clobber forces the reload) instead of ~30 SGPRs of kernel arguments live across the launch
   const DState& st = *reinterpret_cast<const DState*>(mptr + 1);   // DState follows DModel in the header
   (void)stval;
 #else
@@ -940,13 +949,13 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
     for (int c = 0; c < NCLASS; c++) m.cls_start[c + 1] = m.cls_start[c] + ccount[c];
     if (m.npairall > JL * VS * 2) return fail(AW_EUNSUPPORTED, "too many collision pairs");
     PUT(cp_class, pcls); PUT(cp_rb, prb); PUT(cp_margin64, pmg64);
-    // bodies whose fp64 frames the MPR pairs read (stage_kin64): the pairs' bodies + ancestors
-    std::vector<int> k64(nbody, 0);
+    // per MPR pair: the bodies whose fp64 frames its geometry needs (stage_kin64), with ancestors
+    std::vector<unsigned long long> k64(m.npairall, 0ull);
     for (int p = 0; p < m.npairall; p++)
       if (pcls[p] == 4)
         for (int g : {pg1[p], pg2[p]})
-          for (int b = cbody[g]; b > 0; b = parent[b]) k64[b] = 1;
-    PUT(body_kin64, k64);
+          for (int b = cbody[g]; b > 0; b = parent[b]) k64[p] |= 1ull << b;
+    PUT(cp_kin64, k64);
     std::vector<int> ppack(m.npairall);
     for (int p = 0; p < m.npairall; p++) ppack[p] = pcls[p] | (pg1[p] << 8) | (pg2[p] << 16);
     PUT(cp_pack, ppack);

@@ -156,7 +156,7 @@ constexpr int MAXRG = 64;     // rendered (primitive) geoms
   X(double, body_pos64, MAXB * 3) X(double, body_quat64, MAXB * 4) X(double, jnt_pos64, MAXV * 3) \
   X(double, jnt_axis64, MAXV * 3) X(double, geom_pos64, MAXG * 3) X(double, geom_quat64, MAXG * 4) \
   X(double, geom_size64, MAXG * 3) X(double, cp_margin64, MAXPAIR)                                 \
-  X(int, body_kin64, MAXB) /* 1: the body's fp64 frame is needed (ancestor of an MPR geom) */
+  X(unsigned long long, cp_kin64, MAXPAIR) /* bodies of the pair's geoms + their ancestors */
 
 struct MData {
 #define AW_X(T, name, n) T name[n];
@@ -263,6 +263,7 @@ struct __attribute__((aligned(16))) Env {
   float J[JL][VS] __attribute__((aligned(16)));
   float rowbuf[MAXEFC];
   unsigned status;
+  unsigned long long kin64_mask;   // bodies whose fp64 frames this substep's MPR pairs read
   int slot;                   // workgroup slot: selects the dense-J spill and M-factor blocks,
                               // reused by every env the persistent k_step workgroup processes
   int it_newton, it_noslip;   // iterations of the last solve (introspection)

@@ -158,8 +158,9 @@ AW_DEV void apply_ovr64(const DModel& m, const Env& s, int field, int obj, doubl
     }
 }
 
-// mj_kinematics in fp64 for the bodies that carry MPR (cylinder) pair geometry and their
-// ancestors (body_kin64), from the fp32 state with the model's fp64 constants: the oracle's
+// mj_kinematics in fp64 for the bodies that carry the geometry of this substep's MPR (cylinder)
+// pairs and their ancestors (s.kin64_mask), from the fp32 state with the model's fp64 constants
+// (levels holding none of them are skipped): the oracle's
 // operation order (oracle/mjstep.cc kinematics: parent xmat * body_pos, xquat chain, hinge
 // axis-angle quaternions, normalised).  MPR contact points are ill-conditioned on line / face
 // contacts (a cylinder lying on a box: rotating the cylinder by 1e-7 rad moves MuJoCo's point
@@ -171,15 +172,16 @@ AW_DEV void stage_kin64(const DModel& m, Env& s, int lane) {
     X[3] = 1.0; X[4] = X[5] = X[6] = 0.0;
   }
   wsync();
-  const bool own = lane > 0 && lane < m.nbody && MD(body_kin64, lane);
+  const bool own = lane > 0 && lane < m.nbody && ((s.kin64_mask >> lane) & 1ull);
   const int b = own ? lane : 0;
   const int dep = own ? MD(body_depth, b) : -1;
+  const int ntop = (int)wave_max((float)dep) + 1;   // deepest level holding a needed frame
   const int p = MD(body_parentid, b), da = MD(body_dofadr, b), dn = own ? MD(body_dofnum, b) : 0;
   double bp[3], bq[4];
   for (int k = 0; k < 3; k++) bp[k] = MD(body_pos64, 3 * b + k);
   for (int k = 0; k < 4; k++) bq[k] = MD(body_quat64, 4 * b + k);
   if (own && MD(body_ovr, b)) { apply_ovr64<3>(m, s, 0, b, bp); apply_ovr64<4>(m, s, 1, b, bq); }
-  for (int lev = 1; lev < m.nlevel; lev++) {
+  for (int lev = 1; lev < ntop; lev++) {
     if (dep == lev) {
       const double* P = kin64(s, p);
       double pq[4] = {P[3], P[4], P[5], P[6]}, pm[9], xp[3], xq[4];

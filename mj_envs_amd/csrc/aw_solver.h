@@ -29,7 +29,8 @@ namespace aw {
 #ifdef AW_CHOL_READLANE
 // Variant: the column is broadcast with v_readlane (SGPR operands) instead of an LDS round trip.
 template <int NV>
-AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
+AW_DEV void chol_factor(float (&row)[NV], int lane_in, float& invd, Env& s) {
+  const int lane = opaque(lane_in);   // lane compares are made here, not hoisted out of the caller's loop
 #pragma unroll
   for (int j = 0; j < NV; j++) {
     const float djj = fmaxf(rlane(row[j], j), MINVAL);
@@ -49,7 +50,8 @@ AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
 // rest of the rank-1 update (rows > j+LA) reads the column from LDS and lags behind the pivot
 // chain.  Same operands in every fma: bitwise the plain form's factor (A/B -0.35 %, r03d).
 template <int NV>
-AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
+AW_DEV void chol_factor(float (&row)[NV], int lane_in, float& invd, Env& s) {
+  const int lane = opaque(lane_in);   // lane compares are made here, not hoisted out of the caller's loop
   constexpr int LA = AW_CHOL_LA;
   float* col = reinterpret_cast<float*>(s.colbuf);
 #pragma unroll
@@ -82,7 +84,8 @@ AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
 }
 #else
 template <int NV>
-AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
+AW_DEV void chol_factor(float (&row)[NV], int lane_in, float& invd, Env& s) {
+  const int lane = opaque(lane_in);   // lane compares are made here, not hoisted out of the caller's loop
   float* col = reinterpret_cast<float*>(s.colbuf);
 #pragma unroll
   for (int j = 0; j < NV; j++) {
@@ -111,7 +114,8 @@ AW_DEV void chol_factor(float (&row)[NV], int lane, float& invd, Env& s) {
 }
 #endif
 template <int NV>
-AW_DEV void chol_store(const float (&row)[NV], int lane, Env& s) {
+AW_DEV void chol_store(const float (&row)[NV], int lane_in, Env& s) {
+  const int lane = opaque(lane_in);
   if (lane < NV) {
 #pragma unroll
     for (int k = 0; k < NV; k++)
@@ -120,7 +124,8 @@ AW_DEV void chol_store(const float (&row)[NV], int lane, Env& s) {
 }
 // x = inv(L L') b, b lane-distributed; L rows in registers (forward) and packed in LDS (backward)
 template <int NV>
-AW_DEV float chol_solve(const float (&row)[NV], float invd, float b, int lane, const Env& s) {
+AW_DEV float chol_solve(const float (&row)[NV], float invd, float b, int lane_in, const Env& s) {
+  const int lane = opaque(lane_in);
 #pragma unroll
   for (int j = 0; j < NV; j++) {
     float yj = rlane(b, j) * rlane(invd, j);
@@ -534,8 +539,9 @@ AW_DEV void hess_dense_mfma(const DModel& m, Env& s, int lane) {
 #endif
 
 template <int NV>
-AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[NV], float& a, float qfrc_smooth,
+AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mrow)[NV], float& a, float qfrc_smooth,
                          float qacc_smooth) {
+  const int lane = lane_nt;
   const int nefc = s.nefc;
   const float fs = lane < NV ? qfrc_smooth : 0.f;
   const float a0 = lane < NV ? qacc_smooth : 0.f;
@@ -604,6 +610,7 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
   for (int h = 0; h < NRL; h++) inH[h] = false;
   const int li = lane < NV ? lane : NV - 1;
   for (; iter < m.iterations; iter++) {
+    const int lane = opaque(lane_nt);   // per-iteration lane id: its compares stay inside the loop
     float H[NV];
     bool full = iter == 0;
     if (!full) {
@@ -842,7 +849,8 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane, const float (&Mrow)[
 // ---------------------------------------------------------------------------------------
 // noslip: PGS over frictionloss rows and opposing pyramid-edge pairs, no regularisation
 template <int TASK, bool KEEP_D>
-AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[Tree<TASK>::NV], float& qacc) {
+AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mrow)[Tree<TASK>::NV], float& qacc) {
+  const int lane = lane_ns;
   constexpr int NV = Tree<TASK>::NV;
   const int nsparse = s.nsparse, ndense = s.ndense;
   // inv(M) from the tree factor of M (aw_tree.h): lane i keeps row i of inv(M) in VGPRs
@@ -955,6 +963,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane, const float (&Mrow)[
   AW_PROF(s, PR_NS_SETUP);
   if (lane == 0) s.it_noslip = 0;
   for (int it = 0; it < m.noslip_iterations; it++) {
+    const int lane = opaque(lane_ns);   // per-sweep lane id: the dof / pair compares stay in the sweep
     AW_PROF_ADD(s, PR_NOSLIP_IT, 1);
     if (lane == 0) s.it_noslip = it + 1;
     float impr = 0.f;

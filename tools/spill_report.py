@@ -2,7 +2,7 @@
 import collections, re, subprocess, sys
 task = sys.argv[1] if len(sys.argv) > 1 else "0"   # task kind (hammer 0)
 src = "mj_envs_amd/csrc/adroit_wave.hip"
-subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-g", "-S", "--cuda-device-only",
+subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-g", "-S", "--cuda-device-only", "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-fgpu-flush-denormals-to-zero",
                 f"-DAW_ONLY_TASK={task}", "-o", "/tmp/isa/one.s", src], check=True)
 lines = open("/tmp/isa/one.s").readlines()
 fmap = {}

@@ -71,5 +71,45 @@ def main(tag):
                                           "algorithmic_bytes_per_env_step", "write_calibration")}))
 
 
+def sq(tag):
+    """SQ issue / wait split of k_step from the three --pmc passes of tools/gpu_prof.sh"""
+    import collections
+    src = os.path.join(REPO, "gpurun_out", tag)
+    per = {}
+    for f in ("sq1", "sq2", "sq3"):
+        path = os.path.join(src, f, f"{f}_counter_collection.csv")
+        if not os.path.exists(path):
+            return None
+        agg = collections.defaultdict(lambda: collections.defaultdict(float))
+        for r in csv.DictReader(open(path)):
+            if "k_step" in r["Kernel_Name"]:
+                agg[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+        for c, d in agg.items():
+            per[c] = sum(d.values()) / len(d)
+    waves = per["SQ_WAVES"]
+    subs = 65536 * 5 / waves          # wave-substeps per wave (headline launch: 65 536 envs x 5)
+    wc = per["SQ_WAVE_CYCLES"]
+    out = dict(tag=tag, kernel="k_step (hammer-v0, 65 536 envs, persistent grid)", per_dispatch=per,
+               per_wave_substep={k: round(v / waves / subs, 1) for k, v in per.items() if k != "SQ_WAVES"},
+               fractions_of_wave_cycles={k: round(per[c] / wc, 4) for k, c in (
+                   ("active_inst_any", "SQ_ACTIVE_INST_ANY"), ("active_valu", "SQ_ACTIVE_INST_VALU"),
+                   ("active_lds", "SQ_ACTIVE_INST_LDS"), ("wait_any", "SQ_WAIT_ANY"),
+                   ("wait_inst_any", "SQ_WAIT_INST_ANY"), ("wait_inst_lds", "SQ_WAIT_INST_LDS"))},
+               note="SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles (x4 = shader cycles); "
+                    "WAIT_ANY = parked on s_waitcnt, WAIT_INST_ANY = issue stall on a dependency, "
+                    "ACTIVE_INST_ANY = issuing (MI355X_MICROARCH.md PMC section)")
+    with open(os.path.join(REPO, "profiles", f"{tag}_sq_kstep.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    return out
+
+
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
+    t = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    main(t)
+    r = sq(t)
+    if r:
+        print(json.dumps(r["fractions_of_wave_cycles"]))
+    for f in ("stage_profile.json", "stage_profile_dapg.json"):
+        p = os.path.join(REPO, "gpurun_out", t, f)
+        if os.path.exists(p):
+            shutil.copy(p, os.path.join(REPO, "profiles", f"{t}_{f}"))
