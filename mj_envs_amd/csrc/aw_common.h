@@ -168,12 +168,18 @@ struct MData {
 // global_load saddr form (SGPR base, one VGPR offset) instead of a 64-bit per-lane address
 // The table lives in device global memory: reading it through a global-address-space pointer
 // emits global_load (vmcnt only) instead of flat_load, whose completion also holds lgkmcnt and
-// so makes every LDS wait in flight behind it wait for the model read too.
+// so makes every LDS wait in flight behind it wait for the model read too.  The table is read-only
+// for the life of a launch, so it is read through the constant address space (4): a read at a
+// wave-uniform offset becomes a scalar load (no VGPR, no vmcnt), a per-lane one stays a
+// global_load (A/B r03g: -1.1 % k_step against address space 1).
+#ifndef AW_MD_AS
+#define AW_MD_AS 4
+#endif
 #ifndef AW_MD_FLAT
 template <class T>
 AW_DEV T mld(const T* base, unsigned i) {
-  typedef const __attribute__((address_space(1))) T GT;
-  typedef const __attribute__((address_space(1))) char GC;
+  typedef const __attribute__((address_space(AW_MD_AS))) T GT;
+  typedef const __attribute__((address_space(AW_MD_AS))) char GC;
   return *(GT*)((GC*)base + i * (unsigned)sizeof(T));
 }
 #else
@@ -182,7 +188,11 @@ AW_DEV T mld(const T* base, unsigned i) {
   return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + i * (unsigned)sizeof(T));
 }
 #endif
+#ifndef AW_MD_INLINE_LOC
 #define MD(name, idx) ::aw::mld(m.d->name, (unsigned)(idx))
+#else   // analysis builds (tools/isa_regions.py): the load is attributed to the reading line
+#define MD(name, idx) (*(const __attribute__((address_space(1))) __typeof__(m.d->name[0])*)((const __attribute__((address_space(1))) char*)(m.d->name) + (unsigned)(idx) * (unsigned)sizeof(m.d->name[0])))
+#endif
 // device-global views of model / state arrays (global_load / global_store, not flat)
 template <class T> using gp_t = __attribute__((address_space(1))) T*;
 template <class T> AW_DEV gp_t<const T> gcp(const T* p) { return (gp_t<const T>)p; }

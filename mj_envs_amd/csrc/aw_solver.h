@@ -872,15 +872,12 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
   const float lm = lane < NV ? 1.f : 0.f;
   wsync();
   AW_PROF(s, PR_NS_MINV);
-  // forces: frictionloss rows per dof lane, dense rows per lane
+  // forces: frictionloss rows per dof lane, pyramid-edge pairs per pair lane
   const bool use_fl = !(m.disableflags & DSBL_FRICTIONLOSS);
-  float ffl = 0.f, fd = 0.f;
+  float ffl = 0.f;
   // per-dof-lane constants of the frictionloss row of that dof (lane d owns row fl_row[d])
   float fl_aref = 0.f, fl_lim = 0.f, fl_A = 1.f, fl_invA = 0.f;
-  bool fl_ok;
-#ifndef AW_NOSLIP_SLOWCHAIN
   float fl_c = 0.f;   // ffl + aref / A: the proposal is med3(fl_c - qacc / A, -lim, lim)
-#endif
   {
     float dg = 0.f;   // inv(M)[lane][lane]
 #pragma unroll
@@ -888,33 +885,28 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
     const int row = lane < NV ? MD(fl_row, lane) : -1;
     const bool has = row >= 0 && row < nsparse;
     if (has) ffl = s.efc_force[row];
-    fl_ok = use_fl && has && dg >= MINVAL;
-    if (fl_ok) {
+    if (use_fl && has && dg >= MINVAL) {
       fl_aref = s.efc_aref[row];
       fl_lim = s.efc_floss[row];
       fl_A = dg;
       fl_invA = 1.0f / dg;
+    } else {
+      // lanes without an active row propose their own force back (dl = 0 exactly): invA 0, no clamp
+      fl_invA = 0.f;
+      fl_lim = 3.0e38f;
     }
-#ifndef AW_NOSLIP_SLOWCHAIN
-    // lanes without an active row propose their own force back (dl = 0 exactly): invA 0, no clamp
-    if (!fl_ok) { fl_invA = 0.f; fl_lim = 3.0e38f; }
     fl_c = fmaf(fl_aref, fl_invA, ffl);
-#endif
   }
-  // dense-row forces: row lane in fd, row 64 + lane in fd_hi (ndense <= MAXDENSE = 128)
-  float fd_hi = 0.f;
-  if (lane < ndense) fd = s.efc_force[nsparse + lane];
-  if (lane + 64 < ndense) fd_hi = s.efc_force[nsparse + 64 + lane];
   qacc = lane < NV ? qacc : 0.f;
   const float scale = 1.f / (m.meaninertia * (float)(NV > 1 ? NV : 1));
   // opposing pyramid-edge pairs (e, e+1) in row order.  A pair's update keeps f1 + f2 (the
   // normal force) and moves x = f1 - f2, so d2 = -d1 and everything it needs is the difference
   // of its two rows: jd = J_e - J_e+1 and xd = inv(M) jd' (dof vectors), K = jd . xd,
-  // r1 - r2 = jd . qacc - (aref_e - aref_e+1).  Pairs with K >= MINVAL are compacted, pair p's
-  // constants in lane p; jd / xd of the first NSP_CACHE pairs stay in VGPRs, the next NSP_LDS
-  // are parked in dead LDS, the rest are rebuilt each sweep.
+  // r1 - r2 = jd . qacc - (aref_e - aref_e+1).  Pairs with K >= MINVAL are compacted; pair p's
+  // constants and its two forces live in lane p.  jd / xd of the first NSP_CACHE pairs stay in
+  // VGPRs, the next NSP_LDS are parked in dead LDS, the rest are rebuilt each sweep.
   int npr = 0, pr_e = 0;
-  float pr_k = 0.f, pr_ik = 0.f, pr_ard = 0.f;
+  float pr_ik = 0.f, pr_aik = 0.f, pr_ard = 0.f, pr_hk = 0.f, pf1 = 0.f, pf2 = 0.f;
   float c_jd[NSP_CACHE], c_xd[NSP_CACHE];
 #pragma unroll
   for (int p = 0; p < NSP_CACHE; p++) c_jd[p] = c_xd[p] = 0.f;
@@ -935,8 +927,6 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
     }
     xd = a;
   };
-  // dense-row force of row e (uniform)
-  auto fd_get = [&](int e) { return e < 64 ? rlane(fd, e) : rlane(fd_hi, e - 64); };
   for (int e = 0; e + 1 < ndense; e++) {
     if (!(s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1)) continue;
     float jd, xd;
@@ -945,19 +935,49 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
     if (!(K >= MINVAL)) continue;
     const int p = npr++;
     if (lane == p) {
-      pr_e = e; pr_k = K; pr_ik = 1.0f / K;
+      pr_e = e; pr_ik = 1.0f / K; pr_hk = 0.5f * K;
       pr_ard = s.efc_aref[nsparse + e] - s.efc_aref[nsparse + e + 1];
+      pr_aik = pr_ard * pr_ik;
+      pf1 = s.efc_force[nsparse + e];
+      pf2 = s.efc_force[nsparse + e + 1];
     }
 #pragma unroll
     for (int q = 0; q < NSP_CACHE; q++)
       if (q == p) { c_jd[q] = jd; c_xd[q] = xd; }
-#ifndef AW_NOSLIP_NOLDS
     if (p >= NSP_CACHE && p < NSP_CACHE + NSP_LDS<KEEP_D> && lane < MAXV) {
       float* slot = xpark_slot<KEEP_D>(s, p - NSP_CACHE);
       slot[lane] = jd;
       slot[MAXV + lane] = xd;
     }
-#endif
+  }
+  // Pair space of the cached pairs: S (lane q) = jd_q . qacc is the residual that pair q's update
+  // reads, and an update d1 of pair p moves it by G_p d1 with G_p (lane q) = jd_q . xd_p -- a
+  // constant of the solve.  So a pair's step is fma -> med3 -> readlane -> fma on the serial chain
+  // (no wave reduction), and S is recomputed from qacc once per sweep, after the dry-friction rows.
+  const int ncache = npr < NSP_CACHE ? npr : NSP_CACHE;
+  float G[NSP_CACHE];
+  {
+    // lane q < ncache: jd_q at every dof (its two rows, from LDS or the spill block)
+    const bool own = lane < ncache;
+    const int e = own ? pr_e : 0;
+    float jq[NV];
+    if (e + 1 < JL) {
+#pragma unroll
+      for (int d = 0; d < NV; d++) jq[d] = s.J[e][d] - s.J[e + 1][d];
+    } else {
+      auto jat = [&](int r, int d) { return r < JL ? s.J[r][d] : jspill_row(m, s, r)[d]; };
+#pragma unroll
+      for (int d = 0; d < NV; d++) jq[d] = jat(e, d) - jat(e + 1, d);
+    }
+#pragma unroll
+    for (int p = 0; p < NSP_CACHE; p++) {
+      float g = 0.f;
+      if (p < ncache) {
+#pragma unroll
+        for (int d = 0; d < NV; d++) g = fmaf(jq[d], rlane(c_xd[p], d), g);
+      }
+      G[p] = own ? g : 0.f;
+    }
   }
   wsync();
   AW_PROF(s, PR_NS_SETUP);
@@ -966,85 +986,83 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
     const int lane = opaque(lane_ns);   // per-sweep lane id: the dof / pair compares stay in the sweep
     AW_PROF_ADD(s, PR_NOSLIP_IT, 1);
     if (lane == 0) s.it_noslip = it + 1;
-    float impr = 0.f;
     // dry-friction rows in dof order (Gauss-Seidel).  Every lane evaluates the projected update
-    // of its own row against the current qacc; step d keeps lane d's.  Lanes without an
-    // active row propose exactly zero (branch-free).
-    float imp_l = 0.f;
-#ifdef AW_NOSLIP_SLOWCHAIN
-#pragma unroll
-    for (int d = 0; d < NV; d++) {
-      const float r = qacc - fl_aref;
-      const float x = fminf(fmaxf(fmaf(-r, fl_invA, ffl), -fl_lim), fl_lim);
-      const float dl = fl_ok ? x - ffl : 0.f;
-      const float delta = rlane(dl, d);
-      if (lane == d) {
-        imp_l += r * dl + 0.5f * fl_A * dl * dl;
-        ffl = fl_ok ? x : ffl;
-      }
-      qacc = fmaf(Mi[d], delta, qacc);
-    }
-#else
-    // the serial chain per row: fma -> med3 -> sub -> readlane -> fma (was 8 dependent ops)
+    // of its own row against the current qacc; step d keeps lane d's (x and the qacc it saw, for
+    // the force and the improvement after the loop).  Lanes without an active row propose
+    // exactly zero (branch-free).  Serial chain per row: fma -> med3 -> sub -> readlane -> fma.
+    float xsv = ffl, qsv = 0.f;
 #pragma unroll
     for (int d = 0; d < NV; d++) {
       const float x = __builtin_amdgcn_fmed3f(fmaf(-qacc, fl_invA, fl_c), -fl_lim, fl_lim);
-      const float dl = x - ffl;
-      const float delta = rlane(dl, d);
-      if (lane == d) {
-        imp_l += (qacc - fl_aref) * dl + 0.5f * fl_A * dl * dl;
-        ffl = x;
-        fl_c = fmaf(fl_aref, fl_invA, x);
-      }
+      const float delta = rlane(x - ffl, d);
+      if (lane == d) { xsv = x; qsv = qacc; }
       qacc = fmaf(Mi[d], delta, qacc);
     }
-#endif
-    impr -= wave_sum(imp_l);
+    float imp_l;
+    {
+      const float dl = xsv - ffl;
+      imp_l = (qsv - fl_aref) * dl + 0.5f * fl_A * dl * dl;
+      ffl = xsv;
+      fl_c = fmaf(fl_aref, fl_invA, ffl);
+    }
     // opposing pyramid-edge pairs, in row order (branch-free: a zero update is an exact no-op).
-    // One wave reduction per pair on the qacc chain (r1 - r2); d2 = -d1, so the improvement is
-    // (r1 - r2) d1 + K d1^2 / 2 and qacc moves along xd.
-    auto pair_step = [&](int p, float jd, float xd) {
-      const int e = rlane_i(pr_e, p);
-      const float f1 = fd_get(e), f2 = fd_get(e + 1);
-      const float ik = rlane(pr_ik, p), ard = rlane(pr_ard, p);
-      const float sq = wave_sum(jd * qacc);
-      // x' = clamp(x - 2 rd / K, -sum, sum) with x = f1 - f2, sum = f1 + f2 gives
-      // d1 = (x' - x) / 2 = med3(-rd / K, -f1, f2): three ops on the qacc chain after the sum
-      const float d1 = __builtin_amdgcn_fmed3f(fmaf(-sq, ik, ard * ik), -f1, f2);
-      const float rd = sq - ard;
-      const float f1n = f1 + d1, f2n = f2 - d1;
-      impr -= rd * d1 + 0.5f * rlane(pr_k, p) * d1 * d1;
-      qacc = fmaf(xd, d1, qacc);
-      if (e < 64) {
-        if (lane == e) fd = f1n;
-        if (lane == e + 1) fd = f2n;       // e + 1 == 64 lands in no lane of fd ...
-        if (e == 63 && lane == 0) fd_hi = f2n;   // ... but in lane 0 of fd_hi
-      } else {
-        if (lane + 64 == e) fd_hi = f1n;
-        if (lane + 64 == e + 1) fd_hi = f2n;
-      }
-    };
+    // x' = clamp(x - 2 rd / K, -sum, sum) with x = f1 - f2, sum = f1 + f2 gives
+    // d1 = (x' - x) / 2 = med3(-rd / K, -f1, f2); the improvement is rd d1 + K d1^2 / 2.
+    if (ncache > 0) {
+      float S = 0.f;
 #pragma unroll
-    for (int p = 0; p < NSP_CACHE; p++)
-      if (p < npr) pair_step(p, c_jd[p], c_xd[p]);
+      for (int c = 0; c < NSP_CACHE; c += 4) {
+        if (c < ncache) {
+#pragma unroll
+          for (int p = c; p < c + 4 && p < NSP_CACHE; p++) {
+            const float sp = wave_sum(c_jd[p] * qacc);
+            S = lane == p ? sp : S;
+          }
+        }
+      }
+      float d1sv = 0.f, ssv = 0.f;
+#pragma unroll
+      for (int p = 0; p < NSP_CACHE; p++) {
+        if (p < ncache) {
+          const float d1v = __builtin_amdgcn_fmed3f(fmaf(-S, pr_ik, pr_aik), -pf1, pf2);   // lane p's
+          const float d1 = rlane(d1v, p);
+          if (lane == p) { d1sv = d1v; ssv = S; }
+          S = fmaf(G[p], d1, S);
+          qacc = fmaf(c_xd[p], d1, qacc);
+        }
+      }
+      imp_l += (ssv - pr_ard) * d1sv + pr_hk * d1sv * d1sv;
+      pf1 += d1sv;
+      pf2 -= d1sv;
+    }
+    // pairs past the VGPR cache: the residual by a wave reduction
     for (int p = NSP_CACHE; p < npr; p++) {
       float jd, xd;
-#ifndef AW_NOSLIP_NOLDS
       if (p < NSP_CACHE + NSP_LDS<KEEP_D>) {   // parked in LDS
         const float* slot = xpark_slot<KEEP_D>(s, p - NSP_CACHE);
         jd = lane < MAXV ? slot[lane] : 0.f;
         xd = lane < MAXV ? slot[MAXV + lane] : 0.f;
-      } else
-#endif
+      } else {
         pair_rows(rlane_i(pr_e, p), jd, xd);
-      pair_step(p, jd, xd);
+      }
+      const float sq = wave_sum(jd * qacc);
+      const float d1 = __builtin_amdgcn_fmed3f(fmaf(-sq, rlane(pr_ik, p), rlane(pr_aik, p)),
+                                               -rlane(pf1, p), rlane(pf2, p));
+      qacc = fmaf(xd, d1, qacc);
+      if (lane == p) {
+        imp_l += (sq - pr_ard) * d1 + pr_hk * d1 * d1;
+        pf1 += d1;
+        pf2 -= d1;
+      }
     }
-    if (impr * scale < m.noslip_tolerance) break;
+    if (-wave_sum(imp_l) * scale < m.noslip_tolerance) break;
   }
   AW_PROF(s, PR_NS_ITER);
   if (lane < NV && MD(fl_row, lane) >= 0 && MD(fl_row, lane) < nsparse) s.efc_force[MD(fl_row, lane)] = ffl;
-  if (lane < ndense) s.efc_force[nsparse + lane] = fd;
-  if (lane + 64 < ndense) s.efc_force[nsparse + 64 + lane] = fd_hi;
+  if (lane < npr) {
+    s.efc_force[nsparse + pr_e] = pf1;
+    s.efc_force[nsparse + pr_e + 1] = pf2;
+  }
   wsync();
 }
 
