@@ -298,6 +298,13 @@ AW_DEV float rlane(float x, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
 }
 AW_DEV int rlane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+// b in lane l, a in the other lanes: v_cndmask against the constant lane mask 1 << l (an SGPR
+// constant, no v_cmp); l must be a compile-time constant after unrolling
+AW_DEV float sel_lane(float a, float b, int l) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(1ull << l));
+  return r;
+}
 // An opaque copy of a lane-dependent value: values derived from it cannot be hoisted above this
 // point (out of the substep loop) to sit in registers across every stage.
 AW_DEV int opaque(int x) {

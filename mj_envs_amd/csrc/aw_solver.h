@@ -848,6 +848,226 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
 
 // ---------------------------------------------------------------------------------------
 // noslip: PGS over frictionloss rows and opposing pyramid-edge pairs, no regularisation
+#ifndef AW_NOSLIP_PAIRS
+// Row space (default).  mj_solNoSlip is projected Gauss-Seidel over the noslip rows: the
+// frictionloss row of every dof (J = e_d) and the opposing pyramid-edge pairs.  A pair's update
+// keeps f1 + f2 and moves f1 - f2 (d2 = -d1), so it acts through its difference row
+// jd = J_e - J_e+1.  With B stacking those rows, the residuals move through the constant
+// A = B inv(M) B'.  Each lane owns one row -- lanes [0, NV) the dof rows, lanes [NV, NV + npl)
+// the first npl <= 64 - NV pairs -- and keeps that row of A in VGPRs: dof lane d holds
+// inv(M)[d][.] and xd_p[d] = (inv(M) jd_p')[d]; pair lane q holds xd_q[.] and
+// G_q[p] = jd_q . xd_p.  The residual vector R (dof lanes: qacc; pair lanes: jd_q . qacc) then
+// moves by ONE fma per row step, for dof rows and pairs alike: a step is
+// fma -> med3 -> readlane -> fma on the serial chain, and qacc is R's dof lanes at the end.
+// Row constants: y = cb - R ca is the unclamped update, d = med3(y, lo, hi) with
+// lo = -lim - fa, hi = lim + fb (dof rows: fa = f, fb = -f, lim = frictionloss; pairs: fa = f1,
+// fb = f2, lim = 0), and the row's cost change is diag d (d / 2 - y).  Pairs past the lanes
+// (npr > npl, rare) rebuild their column of A every sweep.
+template <int TASK, bool KEEP_D>
+AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mrow)[Tree<TASK>::NV], float& qacc) {
+  const int lane = lane_ns;
+  constexpr int NV = Tree<TASK>::NV;
+  constexpr int NPL = 64 - NV;          // pairs with a lane of their own
+  constexpr int XS = (NV + 3) & ~3;     // row stride of the xd transpose buffer (16-byte rows)
+  static_assert(NPL * XS * sizeof(float) <= offsetof(Env, qpos), "xd transpose buffer exceeds the phase-K/S union");
+  float* Xb = reinterpret_cast<float*>(&s);   // phase-K / phase-S union: dead during noslip
+  const int nsparse = s.nsparse, ndense = s.ndense;
+  // dof columns of this lane's row of A: inv(M) from the tree factor of M (aw_tree.h)
+  float Am[NV];
+  {
+    float row[NV];
+#pragma unroll
+    for (int k = 0; k < NV; k++) row[k] = Mrow[k];
+    float invd;
+    tree_factor<TASK>(row, invd, lane);
+    tree_inverse<TASK>(row, invd, lane, Am);
+  }
+  if (lane >= NV) {
+#pragma unroll
+    for (int k = 0; k < NV; k++) Am[k] = 0.f;
+  }
+  const int li = lane < NV ? lane : 0;
+  const float lm = lane < NV ? 1.f : 0.f;
+  wsync();
+  AW_PROF(s, PR_NS_MINV);
+  // dof rows: lanes without an active frictionloss row propose exactly zero (ca = cb = 0, no clamp)
+  const bool use_fl = !(m.disableflags & DSBL_FRICTIONLOSS);
+  const int flrow = lane < NV ? MD(fl_row, lane) : -1;
+  const bool has_fl = flrow >= 0 && flrow < nsparse;
+  float ca = 0.f, cb = 0.f, lim = 0.f, fa = 0.f, fb = 0.f, diag = 0.f;
+  int rowe = 0;   // pair lanes: the pair's first dense row
+  {
+    float dg = 0.f;   // inv(M)[lane][lane]
+#pragma unroll
+    for (int k = 0; k < NV; k++) dg = k == lane ? Am[k] : dg;
+    if (has_fl) { fa = s.efc_force[flrow]; fb = -fa; }
+    if (use_fl && has_fl && dg >= MINVAL) {
+      ca = 1.0f / dg;
+      cb = s.efc_aref[flrow] * ca;
+      lim = s.efc_floss[flrow];
+      diag = dg;
+    } else if (lane < NV) {
+      lim = 3.0e38f;
+    }
+  }
+  float R = lane < NV ? qacc : 0.f;
+  // column of A for the pair starting at dense row e: col = A[lane][0..NV) . jd (dof lanes: xd,
+  // pair lanes with their dof columns loaded: G_q); jd = J_e - J_e+1 at this lane's dof
+  auto jval = [&](int d) { return lm * (d < JL ? s.J[d][li] : jspill_row(m, s, d)[li]); };
+  auto pair_col = [&](int e, float& jd, float& col) {
+    float a = 0.f;
+    if (e + 1 < JL) {
+#pragma unroll
+      for (int j = 0; j < NV; j++) a = fmaf(Am[j], s.J[e][j] - s.J[e + 1][j], a);
+      jd = lm * (s.J[e][li] - s.J[e + 1][li]);
+    } else {
+      const float dl = jval(e) - jval(e + 1);
+#pragma unroll
+      for (int j = 0; j < NV; j++) a = fmaf(Am[j], rlane(dl, j), a);
+      jd = dl;
+    }
+    col = a;
+  };
+  // pairs with K = jd . xd >= MINVAL, in row order: the first NPL get a lane (constants there, xd
+  // to the transpose buffer), the rest keep their constants in lane p - NPL
+  int npr = 0;
+  int ex_e = 0;
+  float ex_ca = 0.f, ex_cb = 0.f, ex_K = 0.f, ex_fa = 0.f, ex_fb = 0.f;
+  for (int e = 0; e + 1 < ndense; e++) {
+    if (!(s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1)) continue;
+    float jd, xd;
+    pair_col(e, jd, xd);
+    const float K = wave_sum(jd * xd);
+    if (!(K >= MINVAL)) continue;
+    const int p = npr++;
+    const float ik = 1.0f / K;
+    const float ard = s.efc_aref[nsparse + e] - s.efc_aref[nsparse + e + 1];
+    const float f1 = s.efc_force[nsparse + e], f2 = s.efc_force[nsparse + e + 1];
+    if (p < NPL) {
+      const float Sp = wave_sum(jd * R);   // jd . qacc
+      if (lane < NV) Xb[p * XS + lane] = xd;
+      if (lane == NV + p) { rowe = e; ca = ik; cb = ard * ik; diag = K; fa = f1; fb = f2; R = Sp; }
+    } else if (lane == p - NPL) {
+      ex_e = e; ex_ca = ik; ex_cb = ard * ik; ex_K = K; ex_fa = f1; ex_fb = f2;
+    }
+  }
+  const int npl = npr < NPL ? npr : NPL;
+  wsync();
+  // pair lanes: the dof columns of their row, xd_q, from the transpose buffer
+  if (lane >= NV && lane < NV + npl) {
+    const float* xr = Xb + (lane - NV) * XS;
+#pragma unroll
+    for (int q = 0; q < XS / 4; q++) {
+      const float4 v = *reinterpret_cast<const float4*>(xr + 4 * q);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+        if (4 * q + t < NV) Am[4 * q + t] = vv[t];
+    }
+  }
+  wsync();
+  // pair columns of every lane's row: dof lanes read xd_p[lane] back from the transpose buffer;
+  // pair lanes form G_q[p] = jd_q . xd_p from their difference row (registers) and xd_p
+  // (broadcast reads of the buffer)
+  float Ap[NPL];
+#ifdef AW_NS_G_RECOMPUTE
+#pragma unroll
+  for (int p = 0; p < NPL; p++) {
+    if (p < npl) {
+      float jd, col;
+      pair_col(rlane_i(rowe, NV + p), jd, col);
+      Ap[p] = col;
+    }
+  }
+#else
+  {
+    float jq[NV];
+    const int e = lane >= NV && lane < NV + npl ? rowe : 0;
+    if (e + 1 < JL) {
+#pragma unroll
+      for (int d = 0; d < NV; d++) jq[d] = s.J[e][d] - s.J[e + 1][d];
+    } else {
+      auto jat = [&](int r, int d) { return r < JL ? s.J[r][d] : jspill_row(m, s, r)[d]; };
+#pragma unroll
+      for (int d = 0; d < NV; d++) jq[d] = jat(e, d) - jat(e + 1, d);
+    }
+#pragma unroll
+    for (int p = 0; p < NPL; p++) {
+      if (p < npl) {
+        const float* xr = Xb + p * XS;
+        float g = 0.f;
+#pragma unroll
+        for (int q = 0; q < XS / 4; q++) {
+          const float4 v = *reinterpret_cast<const float4*>(xr + 4 * q);
+          const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int t = 0; t < 4; t++)
+            if (4 * q + t < NV) g = fmaf(jq[4 * q + t], vv[t], g);
+        }
+        Ap[p] = lane < NV ? xr[li] : g;
+      }
+    }
+  }
+#endif
+  AW_PROF(s, PR_NS_SETUP);
+  if (lane == 0) s.it_noslip = 0;
+  const float scale = 1.f / (m.meaninertia * (float)(NV > 1 ? NV : 1));
+  for (int it = 0; it < m.noslip_iterations; it++) {
+    const int lane = opaque(lane_ns);   // per-sweep lane id: the row compares stay in the sweep
+    AW_PROF_ADD(s, PR_NOSLIP_IT, 1);
+    if (lane == 0) s.it_noslip = it + 1;
+    const float lo = -lim - fa, hi = lim + fb;
+    float ysv = 0.f;   // this lane's unclamped update at its own step (its bounds hold all sweep)
+    auto step = [&](float a_c, int c) {
+      const float y = fmaf(-R, ca, cb);
+      const float d = rlane(__builtin_amdgcn_fmed3f(y, lo, hi), c);
+#ifdef AW_NS_SELMASK
+      ysv = sel_lane(ysv, y, c);
+#else
+      ysv = lane == c ? y : ysv;
+#endif
+      R = fmaf(a_c, d, R);
+    };
+#pragma unroll
+    for (int c = 0; c < NV; c++) step(Am[c], c);
+#pragma unroll
+    for (int p = 0; p < NPL; p++)
+      if (p < npl) step(Ap[p], NV + p);
+    const float d = __builtin_amdgcn_fmed3f(ysv, lo, hi);
+    float imp = diag * d * (0.5f * d - ysv);
+    fa += d;
+    fb -= d;
+    // pairs past the lanes: their column of A rebuilt, the residual by a wave reduction
+    for (int x = 0; x < npr - NPL; x++) {
+      const int e = rlane_i(ex_e, x);
+      float jd, col;
+      pair_col(e, jd, col);
+      const float y = fmaf(-wave_sum(jd * R), rlane(ex_ca, x), rlane(ex_cb, x));
+      const float d1 = __builtin_amdgcn_fmed3f(y, -rlane(ex_fa, x), rlane(ex_fb, x));
+      R = fmaf(col, d1, R);
+      if (lane == x) {
+        imp += ex_K * d1 * (0.5f * d1 - y);
+        ex_fa += d1;
+        ex_fb -= d1;
+      }
+    }
+    if (-wave_sum(imp) * scale < m.noslip_tolerance) break;
+  }
+  AW_PROF(s, PR_NS_ITER);
+  qacc = lane < NV ? R : 0.f;
+  if (has_fl) s.efc_force[flrow] = fa;
+  if (lane >= NV && lane < NV + npl) {
+    s.efc_force[nsparse + rowe] = fa;
+    s.efc_force[nsparse + rowe + 1] = fb;
+  }
+  if (lane < npr - NPL) {
+    s.efc_force[nsparse + ex_e] = ex_fa;
+    s.efc_force[nsparse + ex_e + 1] = ex_fb;
+  }
+  wsync();
+}
+#else
+// Pair space (A/B variant, -DAW_NOSLIP_PAIRS).
 template <int TASK, bool KEEP_D>
 AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mrow)[Tree<TASK>::NV], float& qacc) {
   const int lane = lane_ns;
@@ -1065,6 +1285,8 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
   }
   wsync();
 }
+
+#endif
 
 // ---------------------------------------------------------------------------------------
 // mju_rayGeom for site shapes: distance to the first crossing at t >= 0, or -1
