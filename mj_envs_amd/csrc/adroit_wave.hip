@@ -774,6 +774,8 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
 
   std::vector<int> parent = B.i("body_parentid"), rootid = B.i("body_rootid"), dofnum = B.i("body_dofnum"),
                    dofadr = B.i("body_dofadr");
+  for (int b = 0; b < nbody; b++)
+    if (dofnum[b] > MAXJB) return fail(AW_EUNSUPPORTED, "more than MAXJB joints in one body");
   // subtree ends (DFS order), levels, dof masks
   std::vector<int> send(nbody), depth(nbody, 0);
   for (int b = 0; b < nbody; b++) send[b] = b + 1;

@@ -25,6 +25,7 @@ constexpr int MAXU = 30;      // actuators
 // (nconmax 100 / njmax 500, DAPG_assets.xml:4) under the reference's pretrained DAPG policies
 // (profiles/work_counts_*_dapg.json: max ncon 20, nefc 130, dense rows 98 over 4 tasks x 32
 // envs x one horizon): 2.4x / 1.5x / 1.3x headroom.  Overflow still raises ST_*_OVERFLOW.
+constexpr int MAXJB = 6;      // joints of one body (the free objects' 3 slides + 3 hinges)
 constexpr int MAXCON = 48;    // contacts per env (one lane each in the sort)
 constexpr int NRL = 3;        // constraint rows per lane in the Newton solver
 constexpr int MAXEFC = 64 * NRL;  // constraint rows (192)

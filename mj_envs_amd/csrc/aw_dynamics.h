@@ -9,6 +9,11 @@
 
 namespace aw {
 
+// subtree sums over DFS ranges: the loads of this many bodies are issued together
+#ifndef AW_SUB_UNROLL
+#define AW_SUB_UNROLL 4
+#endif
+
 // ---------------------------------------------------------------------------------------
 // this env's parameters + the per-env copies of the overridable fields read in hot loops
 // (geom_size: every collider; body_mass: subtree sums); other overrides are applied where
@@ -48,6 +53,95 @@ AW_DEV void stage_kinematics(const DModel& m, Env& s, int lane) {
     s.xquat[0][0] = 1; s.xquat[0][1] = s.xquat[0][2] = s.xquat[0][3] = 0;
   }
   wsync();
+#ifndef AW_KIN_LEVEL
+  // Body frames without a level sweep.  (A) Lane b composes its body offset and its joints into
+  // ONE rigid transform T_b in the parent's frame -- every lane at once, nothing read from another
+  // lane -- and leaves its joints' axes / anchors in that frame.  (B) Global frames by pointer
+  // jumping on the tree: each round replaces (T, target) with (T_target o T, target's target),
+  // so the dependent chain is log2(depth) compositions instead of depth.  (C) Lane = dof: the
+  // joint axes / anchors to the world frame with the parent's global frame.  Same transforms as
+  // mj_kinematics, composed in a different order (fp32 rounding only).
+  {
+    const bool own = lane > 0 && lane < m.nbody;
+    const int b = own ? lane : 0;
+    const int p = MD(body_parentid, b), da = MD(body_dofadr, b), dn = own ? MD(body_dofnum, b) : 0;
+    float tp[3], tq[4];
+    for (int k = 0; k < 3; k++) tp[k] = MD(body_pos, 3 * b + k);
+    for (int k = 0; k < 4; k++) tq[k] = MD(body_quat, 4 * b + k);
+    if (own && MD(body_ovr, b)) { apply_ovr<3>(m, s, 0, b, tp); apply_ovr<4>(m, s, 1, b, tq); }
+    // (A) branch-free joint steps: a slide is a hinge with ql = 1 and no anchor arm (exact)
+#pragma unroll
+    for (int k = 0; k < MAXJB; k++) {
+      if (k < dn) {
+        const int j = da + k;
+        float axis[3], jp[3], xa[3], xn[3];
+        for (int c = 0; c < 3; c++) { axis[c] = MD(jnt_axis, 3 * j + c); jp[c] = MD(jnt_pos, 3 * j + c); }
+        const bool hinge = MD(jnt_type, j) != JNT_SLIDE;
+        const float q = s.qpos[j];
+        rotvq(xa, axis, tq);
+        rotvq(xn, jp, tq);
+        add3(xn, xn, tp);
+        copy3(s.xaxis[j], xa);    // parent frame; (C) makes them global
+        copy3(s.xanchor[j], xn);
+        // hardware v_sin / v_cos on the half angle reduced to [-pi, pi] (see AW_KIN_LEVEL below)
+        const float hq = hinge ? 0.5f * q : 0.f;
+        const float hr = fmaf(-6.28318530717958648f, rintf(hq * 0.159154943091895336f), hq);
+        const float sn = __sinf(hr), cs = __cosf(hr);
+        const float ql[4] = {cs, axis[0] * sn, axis[1] * sn, axis[2] * sn};
+        mulq(tq, tq, ql);
+        float v[3];
+        rotvq(v, jp, tq);
+        for (int c = 0; c < 3; c++) tp[c] = hinge ? xn[c] - v[c] : fmaf(xa[c], q, tp[c]);
+      }
+    }
+    // (B) pointer jumping; targets in the (not yet written) cinert storage
+    int* tgt = reinterpret_cast<int*>(&s.cinert[0][0]);
+    int t = own ? p : 0;
+    if (own) {
+      copy3(s.xpos[b], tp);
+      for (int c = 0; c < 4; c++) s.xquat[b][c] = tq[c];
+    }
+    if (lane < m.nbody) tgt[lane] = t;
+    wsync();
+    while (__ballot(t != 0)) {
+      float pp[3], pq[4];
+      int tt = 0;
+      if (t != 0) {
+        copy3(pp, s.xpos[t]);
+        for (int c = 0; c < 4; c++) pq[c] = s.xquat[t][c];
+        tt = tgt[t];
+      }
+      wsync();
+      if (t != 0) {
+        float v[3];
+        rotvq(v, tp, pq);
+        add3(tp, pp, v);
+        mulq(tq, pq, tq);
+        t = tt;
+        copy3(s.xpos[b], tp);
+        for (int c = 0; c < 4; c++) s.xquat[b][c] = tq[c];
+        tgt[b] = t;
+      }
+      wsync();
+    }
+    if (own) {
+      normq(tq);
+      for (int c = 0; c < 4; c++) s.xquat[b][c] = tq[c];
+    }
+    wsync();
+    // (C) joint axes / anchors to the world frame (lane = dof)
+    if (lane < m.nv) {
+      const int j = lane, pb = MD(body_parentid, MD(dof_bodyid, j));
+      float pq[4], v[3];
+      for (int c = 0; c < 4; c++) pq[c] = s.xquat[pb][c];
+      rotvq(v, s.xaxis[j], pq);
+      copy3(s.xaxis[j], v);
+      rotvq(v, s.xanchor[j], pq);
+      add3(s.xanchor[j], v, s.xpos[pb]);
+    }
+    wsync();
+  }
+#else
   // lane b owns body b (nbody <= 64) and works at its tree level; its model data (and its first
   // joint's) are loaded once before the level sweep, so a level costs LDS reads of the parent
   // frame + arithmetic, not a chain of dependent model loads
@@ -109,6 +203,7 @@ AW_DEV void stage_kinematics(const DModel& m, Env& s, int lane) {
     }
     wsync();
   }
+#endif
   // geoms (compact collidable list), sites, inertial frames
   for (int g = lane; g < m.ngeom; g += 64) {
     int b = MD(geom_bodyid, g);
@@ -223,7 +318,9 @@ AW_DEV void stage_kin64(const DModel& m, Env& s, int lane) {
 AW_DEV void stage_com(const DModel& m, Env& s, int lane) {
   for (int b = lane; b < m.nbody; b += 64) {
     float acc[3] = {0, 0, 0};
-    for (int d = b; d < MD(body_subtree_end, b); d++) {
+    const int de = MD(body_subtree_end, b);
+#pragma unroll AW_SUB_UNROLL
+    for (int d = b; d < de; d++) {
       float md = s.bmass[d];
       acc[0] += md * s.xipos[d][0]; acc[1] += md * s.xipos[d][1]; acc[2] += md * s.xipos[d][2];
     }
@@ -281,6 +378,7 @@ AW_DEV void stage_crb(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
   for (int k = 0; k < 10; k++) acc[k] = 0;
   const int bb = lane < m.nbody ? lane : 0;
   if (lane < m.nbody && lane > 0)
+#pragma unroll AW_SUB_UNROLL
     for (int d = bb; d < MD(body_subtree_end, bb); d++)
       for (int k = 0; k < 10; k++) acc[k] += s.cinert[d][k];
   wsync();
@@ -319,6 +417,61 @@ AW_DEV float stage_velocity(const DModel& m, Env& s, int lane) {
     if (!(m.disableflags & DSBL_GRAVITY)) { cacc[0][3] = -m.gravity[0]; cacc[0][4] = -m.gravity[1]; cacc[0][5] = -m.gravity[2]; }
   }
   wsync();
+#ifndef AW_RNE_LEVEL
+  // cvel / cacc as tree prefix sums (pointer jumping, log2(depth) rounds) of per-body local terms:
+  // cvel_b = cvel_parent + sum_j cdof_j qvel_j; cacc_b = cacc_parent + sum_j (cv_j x cdof_j) qvel_j
+  // with cv_j the velocity before joint j (mj_comVel's per-joint order inside the body)
+  {
+    const bool own = lane > 0 && lane < m.nbody;
+    const int b = own ? lane : 0;
+    const int p = MD(body_parentid, b), da = MD(body_dofadr, b), dn = own ? MD(body_dofnum, b) : 0;
+    int* tgt = reinterpret_cast<int*>(s.rowbuf);   // dead until the constraint rows
+    auto tree_prefix = [&](float (*arr)[6], float (&v)[6]) {
+      int t = own ? p : -1;
+      if (own)
+        for (int k = 0; k < 6; k++) arr[b][k] = v[k];
+      if (lane < m.nbody) tgt[lane] = t;
+      wsync();
+      while (__ballot(t >= 0)) {
+        float u[6];
+        int tt = -1;
+        if (t >= 0) {
+          for (int k = 0; k < 6; k++) u[k] = arr[t][k];
+          tt = tgt[t];
+        }
+        wsync();
+        if (t >= 0) {
+          for (int k = 0; k < 6; k++) { v[k] += u[k]; arr[b][k] = v[k]; }
+          tgt[b] = tt;
+          t = tt;
+        }
+        wsync();
+      }
+    };
+    float lv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < MAXJB; k++)
+      if (k < dn) {
+        const int j = da + k;
+        const float qv = s.qvel[j];
+        for (int c = 0; c < 6; c++) lv[c] = fmaf(s.cdof[j][c], qv, lv[c]);
+      }
+    tree_prefix(cvel, lv);
+    float w[6], la[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < 6; c++) w[c] = cvel[p][c];
+#pragma unroll
+    for (int k = 0; k < MAXJB; k++)
+      if (k < dn) {
+        const int j = da + k;
+        float cd[6], cdd[6];
+        const float qv = s.qvel[j];
+        for (int c = 0; c < 6; c++) cd[c] = s.cdof[j][c];
+        cross_motion(cdd, w, cd);
+        for (int c = 0; c < 6; c++) { la[c] = fmaf(cdd[c], qv, la[c]); w[c] = fmaf(cd[c], qv, w[c]); }
+      }
+    tree_prefix(cacc, la);
+  }
+#else
   {
     // lane b owns body b at its tree level (as in stage_kinematics)
     const bool own = lane > 0 && lane < m.nbody;
@@ -341,6 +494,7 @@ AW_DEV float stage_velocity(const DModel& m, Env& s, int lane) {
       wsync();
     }
   }
+#endif
   // local body force: cinert*cacc + cvel x* (cinert*cvel), written over cacc
   for (int b = 1 + lane; b < m.nbody; b += 64) {
     float f[6], t1[6], t2[6];
@@ -357,6 +511,7 @@ AW_DEV float stage_velocity(const DModel& m, Env& s, int lane) {
   const int bb = lane < m.nbody ? lane : 0;
   for (int k = 0; k < 6; k++) sub[k] = 0;
   if (lane < m.nbody && lane > 0)
+#pragma unroll AW_SUB_UNROLL
     for (int d = bb; d < MD(body_subtree_end, bb); d++)
       for (int k = 0; k < 6; k++) sub[k] += cacc[d][k];
   wsync();

@@ -4,13 +4,14 @@
 // mj_Euler (fp64 statement: oracle/solver.cc, oracle/mjstep.cc).  Layout on the wave:
 //   * rows [0, nsparse): frictionloss / joint-limit / tendon-limit rows with <= 2 nonzeros,
 //     kept as (index, value) pairs; rows [nsparse, nefc): contact rows, dense J in LDS.
-//   * Newton: lane i holds row i of H = M + J'DJ in VGPRs; H is factored in registers
-//     (v_readlane broadcasts), the factor is written once to LDS for the backward solve.
-//   * rows are evaluated lane-per-row (two rows per lane, nefc <= 128); the exact line search
+//   * Newton: lane i holds row i of H = M + J'DJ in VGPRs; the dense part J_d'DJ_d is formed on
+//     the matrix cores (v_mfma_f32_16x16x4_f32), H is factored as U D U' in registers (column
+//     broadcast through LDS), the factor is written once to LDS for the backward substitution.
+//   * rows are evaluated lane-per-row (three rows per lane, nefc <= 192); the exact line search
 //     and the cost are wave reductions.
-//   * noslip: lane k holds row k of inv(M) and of X = inv(M) J_edges' (<= 64 edges) in VGPRs,
-//     so each PGS update is a handful of broadcasts + one FMA per lane; qacc is kept current
-//     instead of a dual residual matrix.
+//   * noslip: projected Gauss-Seidel in row space -- lane k owns noslip row k (dof frictionloss
+//     rows, then pyramid-edge pairs) and holds its row of A = B inv(M) B' in VGPRs, so a row's
+//     update is fma -> med3 -> readlane -> fma on the serial chain.
 #pragma once
 #include "aw_common.h"
 #include "aw_tree.h"
@@ -18,7 +19,7 @@
 namespace aw {
 
 // ---------------------------------------------------------------------------------------
-// dense Cholesky of a lane-distributed SPD matrix (lane i holds row i; lower part used).
+// dense factorisation of a lane-distributed SPD matrix (lane i holds row i; lower part used).
 // Right-looking: column j is scaled in registers, published once through LDS, and every lane
 // pulls the column back with 16-byte broadcast reads for its rank-1 update.  Entries above a
 // lane's diagonal (and rows of lanes >= NV) take unmasked garbage updates that are never read:
@@ -26,6 +27,72 @@ namespace aw {
 #ifndef AW_CHOL_LA
 #define AW_CHOL_LA 2
 #endif
+#ifndef AW_CHOL_LLT
+// LDL' (default): H = U D U' with U unit lower triangular, right-looking with look-ahead.  Column
+// j: pivot D_j = H'_jj (clamped at MINVAL like mju_cholFactor's diagonal), U_ij = H'_ij / D_j; the
+// rank-1 update H'_ik -= H'_ij U_kj takes the lane's own unscaled entry and the published scaled
+// column.  Every entry on or above a lane's diagonal ends as exactly 0 (U's unit diagonal is
+// implicit, 1 / D_j is kept in lane j's invd), so the substitutions below run unmasked: one
+// readlane -> fma per step, no pivot scaling on the chain.
+template <int NV>
+AW_DEV void chol_factor(float (&row)[NV], int lane_in, float& invd, Env& s) {
+  const int lane = opaque(lane_in);   // lane compares are made here, not hoisted out of the caller's loop
+  constexpr int LA = AW_CHOL_LA;
+  float* col = reinterpret_cast<float*>(s.colbuf);
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    const float dj = __builtin_amdgcn_fmed3f(rlane(row[j], j), MINVAL, 3.402823466e38f);
+    const float inv = __builtin_amdgcn_rcpf(dj);
+    if (lane == j) invd = inv;
+    const float a = row[j];                     // H'_ij, unscaled
+    const float u = lane > j ? a * inv : 0.f;   // U_ij below the diagonal, 0 on and above it
+    row[j] = u;
+#pragma unroll
+    for (int t = 1; t <= LA; t++)
+      if (j + t < NV) row[j + t] = fmaf(-a, rlane(u, j + t), row[j + t]);
+    if (j + LA + 1 < NV) {
+      col[lane] = u;
+      wsync();
+#pragma unroll
+      for (int q = (j + LA + 1) >> 2; q <= (NV - 1) >> 2; q++) {
+        const float4 c = s.colbuf[q];
+        const float cv[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+          const int k = 4 * q + t;
+          if (k > j + LA && k < NV) row[k] = fmaf(-a, cv[t], row[k]);
+        }
+      }
+      wsync();
+    }
+  }
+}
+// packed rows of U into s.L (row padding included: the factor-reuse path reloads whole 4-blocks)
+template <int NV>
+AW_DEV void chol_store(const float (&row)[NV], int lane_in, Env& s) {
+  const int lane = opaque(lane_in);
+  if (lane < NV) {
+#pragma unroll
+    for (int k = 0; k < NV; k++)
+      if (k <= (lane | 3)) s.L[tri(lane) + k] = row[k];
+  }
+}
+// x = inv(U D U') b, b lane-distributed; U rows in registers (forward) and packed in LDS (backward)
+template <int NV>
+AW_DEV float chol_solve(const float (&row)[NV], float invd, float b, int lane_in, const Env& s) {
+  const int lane = opaque(lane_in);
+#pragma unroll
+  for (int j = 0; j < NV; j++) b = fmaf(-row[j], rlane(b, j), b);
+  b *= invd;
+  const int lc = lane < NV ? lane : 0;
+#pragma unroll
+  for (int j = NV - 1; j > 0; j--) {
+    const float c = s.L[tri(j) + lc];
+    b = fmaf(lane < j ? -c : 0.f, rlane(b, j), b);
+  }
+  return lane < NV ? b : 0.f;
+}
+#else
 #ifdef AW_CHOL_READLANE
 // Variant: the column is broadcast with v_readlane (SGPR operands) instead of an LDS round trip.
 template <int NV>
@@ -33,7 +100,7 @@ AW_DEV void chol_factor(float (&row)[NV], int lane_in, float& invd, Env& s) {
   const int lane = opaque(lane_in);   // lane compares are made here, not hoisted out of the caller's loop
 #pragma unroll
   for (int j = 0; j < NV; j++) {
-    const float djj = fmaxf(rlane(row[j], j), MINVAL);
+    const float djj = __builtin_amdgcn_fmed3f(rlane(row[j], j), MINVAL, 3.402823466e38f);   // max(d, MINVAL) without the canonicalising v_max
     const float inv = __builtin_amdgcn_rsqf(djj);
     const float sq = djj * inv;
     row[j] = lane == j ? sq : row[j] * inv;
@@ -56,7 +123,7 @@ AW_DEV void chol_factor(float (&row)[NV], int lane_in, float& invd, Env& s) {
   float* col = reinterpret_cast<float*>(s.colbuf);
 #pragma unroll
   for (int j = 0; j < NV; j++) {
-    const float djj = fmaxf(rlane(row[j], j), MINVAL);
+    const float djj = __builtin_amdgcn_fmed3f(rlane(row[j], j), MINVAL, 3.402823466e38f);   // max(d, MINVAL) without the canonicalising v_max
     const float inv = __builtin_amdgcn_rsqf(djj);
     const float sq = djj * inv;
     row[j] = lane == j ? sq : row[j] * inv;
@@ -89,7 +156,7 @@ AW_DEV void chol_factor(float (&row)[NV], int lane_in, float& invd, Env& s) {
   float* col = reinterpret_cast<float*>(s.colbuf);
 #pragma unroll
   for (int j = 0; j < NV; j++) {
-    const float djj = fmaxf(rlane(row[j], j), MINVAL);
+    const float djj = __builtin_amdgcn_fmed3f(rlane(row[j], j), MINVAL, 3.402823466e38f);   // max(d, MINVAL) without the canonicalising v_max
     const float inv = __builtin_amdgcn_rsqf(djj);   // v_rsq_f32: one op on the column's critical path
     const float sq = djj * inv;
     row[j] = lane == j ? sq : row[j] * inv;
@@ -139,6 +206,21 @@ AW_DEV float chol_solve(const float (&row)[NV], float invd, float b, int lane_in
     else if (lane < j) b = fmaf(-s.L[tri(j) + lane], xj, b);
   }
   return lane < NV ? b : 0.f;
+}
+#endif   // AW_CHOL_LLT
+// y = M x with M lane-distributed rows and x in LDS (broadcast reads)
+template <int NV>
+AW_DEV float matvec_lds(const float (&row)[NV], const float* x) {
+  float acc = 0.f;
+#pragma unroll
+  for (int q = 0; q < (NV + 3) / 4; q++) {
+    const float4 v = *reinterpret_cast<const float4*>(x + 4 * q);
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+      if (4 * q + t < NV) acc = fmaf(row[4 * q + t], vv[t], acc);
+  }
+  return acc;
 }
 // y = M x with M lane-distributed rows and x lane-distributed
 template <int NV>
@@ -219,10 +301,17 @@ AW_DEV float jt_mul(const DModel& m, Env& s, int lane) {
   const int li = lane < NV ? lane : NV - 1;
   float out = s.vec2[li];
   const int nd = s.ndense, ndl = nd < JL ? nd : JL;
+  // unrolled by 4: the loads of four rows are issued before their fmas (one load latency per
+  // four rows, not per row; the spill rows are global loads)
+#ifndef AW_JT_UNROLL
+#define AW_JT_UNROLL 4
+#endif
+#pragma unroll AW_JT_UNROLL
   for (int d = 0; d < ndl; d++) out = fmaf(s.J[d][li], s.rowbuf[s.nsparse + d], out);
   if (nd > JL) {
     gp_t<const float> Jg = jspill_row(m, s, JL);
-    for (int d = JL; d < nd; d++, Jg += VS) out = fmaf(Jg[li], s.rowbuf[s.nsparse + d], out);
+#pragma unroll AW_JT_UNROLL
+    for (int d = JL; d < nd; d++) out = fmaf(Jg[(d - JL) * VS + li], s.rowbuf[s.nsparse + d], out);
   }
   return lane < NV ? out : 0.f;
 }
@@ -467,54 +556,55 @@ AW_DEV float row_eval(const RowR& r, float jar, float* force, int* st) {
   *force = 0.f; *st = S_SAT; return 0.f;
 }
 
-#ifdef AW_HESS_MFMA
+#ifndef AW_HESS_VALU
 // J_d' diag(w) J_d over the dense rows (weights w_d in s.rowbuf[nsparse + d], 0 for rows outside
-// the quadratic zone) written into the packed lower triangle s.L.  v_mfma_f32_16x16x4_f32 takes
-// four rows per K-step: lane l supplies A[i = l&15][k = l>>4] = w_d J[d][16 ti + i] and
-// B[k][j = l&15] = J[d][16 tj + j] with d = d0 + (l>>4); accumulator register r of lane l is
-// entry (16 ti + 4 (l>>4) + r, 16 tj + (l&15)).  Tiles (0,0), (1,0), (1,1) cover rows < 32;
-// columns >= 32 (hammer 33, relocate 36) are accumulated on the VALU, lane = row, and rows >= 32
-// take their entries left of column 32 from lanes < 32 by symmetry.
+// the quadratic zone) on the matrix cores, written into the packed lower triangle s.L (default;
+// -DAW_HESS_VALU: rank-1 VALU updates per row).  v_mfma_f32_16x16x4_f32 takes four rows per
+// K-step: lane l supplies A[i = l&15][k = l>>4] = w_d J[d][16 ti + i] and B[k][j = l&15] =
+// J[d][16 tj + j] with d = d0 + (l>>4); accumulator register r of lane l is entry
+// (16 ti + 4 (l>>4) + r, 16 tj + (l&15)).  Tiles (0,0), (1,0), (1,1) cover rows < 32 and, for
+// NV > 32 (hammer 33, relocate 36), (2,0), (2,1), (2,2) the rows from 32.  An MFMA is a k-ordered
+// fp32 fma chain, so the dense part is bitwise the per-row rank-1 updates.  The next K-step's four
+// operands are loaded before this step's MFMAs (LDS rows, or the global spill block past JL): the
+// row loop no longer waits on a load per row.
 template <int NV>
 AW_DEV void hess_dense_mfma(const DModel& m, Env& s, int lane) {
   typedef float f4 __attribute__((ext_vector_type(4)));
-  constexpr int NX = NV > 32 ? NV - 32 : 0;
+  constexpr bool X2 = NV > 32;
   const int nd = s.ndense, ns = s.nsparse;
   const int sub = lane >> 4, col = lane & 15;
-  const int li = lane < NV ? lane : NV - 1;
-  f4 c00 = {0.f, 0.f, 0.f, 0.f}, c10 = c00, c11 = c00;
-  float hx[NX > 0 ? NX : 1];
-#pragma unroll
-  for (int k = 0; k < NX; k++) hx[k] = 0.f;
-  for (int d0 = 0; d0 < nd; d0 += 4) {
+  f4 c00 = {0.f, 0.f, 0.f, 0.f}, c10 = c00, c11 = c00, c20 = c00, c21 = c00, c22 = c00;
+  auto load = [&](int d0, float& w, float& b0, float& b1, float& b2) {
     const int d = d0 + sub;
-    const float w = d < nd ? s.rowbuf[ns + d] : 0.f;
-    if (__ballot(w != 0.f) == 0ull) continue;
-    const int dd = d < nd ? d : nd - 1;
+    const bool v = d < nd;
+    const int dd = v ? d : d0;   // a row of this K-step (d0 < nd): in the same storage as the rest
     // JL is a multiple of 4: a K-step's rows are all in LDS or all in the spill block
     const float* Jr = d0 < JL ? &s.J[dd][0] : (const float*)jspill_row(m, s, dd);
-    float b0 = Jr[col], b1 = Jr[16 + col];
-    b0 = w != 0.f ? b0 : 0.f;
-    b1 = (w != 0.f && 16 + col < NV) ? b1 : 0.f;
-    c00 = __builtin_amdgcn_mfma_f32_16x16x4f32(w * b0, b0, c00, 0, 0, 0);
-    c10 = __builtin_amdgcn_mfma_f32_16x16x4f32(w * b1, b0, c10, 0, 0, 0);
-    c11 = __builtin_amdgcn_mfma_f32_16x16x4f32(w * b1, b1, c11, 0, 0, 0);
-    if (NX > 0) {
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int dq = d0 + q;
-        if (dq >= nd) break;
-        const float wq = s.rowbuf[ns + dq];
-        if (wq == 0.f) continue;
-        const float* Jq = d0 < JL ? &s.J[dq][0] : (const float*)jspill_row(m, s, dq);
-        const float jl = Jq[li];
-        const float av = wq * jl;
-#pragma unroll
-        for (int k = 0; k < NX; k++) hx[k] = fmaf(av, rlane(jl, 32 + k), hx[k]);
-      }
+    w = v ? s.rowbuf[ns + dd] : 0.f;
+    b0 = Jr[col];
+    b1 = Jr[16 + col];
+    b1 = 16 + col < NV ? b1 : 0.f;
+    b2 = X2 ? Jr[32 + (col & 3)] : 0.f;
+    b2 = 32 + col < NV ? b2 : 0.f;
+  };
+  float w = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f;
+  if (nd > 0) load(0, w, b0, b1, b2);
+  for (int d0 = 0; d0 < nd; d0 += 4) {
+    float wn = 0.f, b0n = 0.f, b1n = 0.f, b2n = 0.f;
+    if (d0 + 4 < nd) load(d0 + 4, wn, b0n, b1n, b2n);
+    const float a0 = w * b0, a1 = w * b1;
+    c00 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, c00, 0, 0, 0);
+    c10 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, c10, 0, 0, 0);
+    c11 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, c11, 0, 0, 0);
+    if (X2) {
+      const float a2 = w * b2;
+      c20 = __builtin_amdgcn_mfma_f32_16x16x4f32(a2, b0, c20, 0, 0, 0);
+      c21 = __builtin_amdgcn_mfma_f32_16x16x4f32(a2, b1, c21, 0, 0, 0);
+      c22 = __builtin_amdgcn_mfma_f32_16x16x4f32(a2, b2, c22, 0, 0, 0);
     }
+    w = wn; b0 = b0n; b1 = b1n; b2 = b2n;
   }
-  // lower triangle + row padding (entries j <= (i | 3)) of rows < 32 from the tiles
+  // lower triangle + row padding (entries j <= (i | 3)) of every row, each written once
   auto put = [&](const f4& c, int ti, int tj) {
 #pragma unroll
     for (int r = 0; r < 4; r++) {
@@ -525,15 +615,10 @@ AW_DEV void hess_dense_mfma(const DModel& m, Env& s, int lane) {
   put(c00, 0, 0);
   put(c10, 1, 0);
   put(c11, 1, 1);
-  if (NX > 0) {
-    if (lane < 32) {
-#pragma unroll
-      for (int k = 0; k < NX; k++) s.L[tri(32 + k) + lane] = hx[k];   // H[32+k][lane] = H[lane][32+k]
-    } else if (lane < NV) {
-#pragma unroll
-      for (int k = 0; k < 4; k++)
-        if (32 + k <= (lane | 3)) s.L[tri(lane) + 32 + k] = k < NX ? hx[k < NX ? k : 0] : 0.f;
-    }
+  if (X2) {
+    put(c20, 2, 0);
+    put(c21, 2, 1);
+    put(c22, 2, 2);
   }
 }
 #endif
@@ -562,9 +647,9 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
   float Ma;
   auto set_point = [&](float x) {
     a = lane < NV ? x : 0.f;
-    Ma = matvec<NV>(Mrow, a);
     if (lane < NV) s.vec[lane] = a;
     wsync();
+    Ma = matvec_lds<NV>(Mrow, s.vec);
 #pragma unroll
     for (int h = 0; h < NRL; h++) {
       int r = lane + 64 * h;
@@ -684,12 +769,10 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
     // with 16-byte reads -- a two-dof tendon row's off-diagonal term lands in ONE entry, where
     // adding it in registers took a 2 x NV select chain per row.  Dense rows: rank-1 updates
     // with the row broadcast from LDS.
-#ifdef AW_HESS_MFMA
-    // Dense part J_d' D J_d on the matrix cores (v_mfma_f32_16x16x4_f32, exact fp32): four dense
-    // rows per MFMA K-step into the lower 16x16 tiles of the leading 32x32 block; columns >= 32
-    // (NV > 32) on the VALU with the lane holding the row.  Every lower-triangle entry (and the
-    // row padding) of s.L is written by exactly one plain store, then the sparse rows are added
-    // with LDS atomics as below.
+#ifndef AW_HESS_VALU
+    // Dense part J_d' D J_d on the matrix cores (hess_dense_mfma above): every lower-triangle
+    // entry (and the row padding) of s.L is written by exactly one plain store, then the sparse
+    // rows are added with LDS atomics as below.
 #pragma unroll
     for (int h = 0; h < NRL; h++) {
       int r = lane + 64 * h;
@@ -711,7 +794,7 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
       int r = lane + 64 * h;
       if (r < nefc) {
         float w = rr[h].st == S_QUAD ? rr[h].D : 0.f;
-#ifndef AW_HESS_MFMA
+#ifdef AW_HESS_VALU
         s.rowbuf[r] = w;
 #endif
         if (r < s.nsparse && w != 0.f) {
@@ -741,7 +824,7 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
     }
 #endif
     AW_PROF(s, PR_NT_HOFFD);
-#ifndef AW_HESS_MFMA
+#ifdef AW_HESS_VALU
     const int nd = s.ndense, ndl = nd < JL ? nd : JL;
     for (int d = 0; d < ndl; d++) {
       float w = s.rowbuf[s.nsparse + d];
@@ -775,11 +858,11 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
     float p = -chol_solve<NV>(H, invd, grad, lane, s);
     AW_PROF(s, PR_NT_SOLVE);
     // exact line search on the piecewise-quadratic 1-D cost
-    float Mp = matvec<NV>(Mrow, p);
-    float c0 = wave_sum(lane < NV ? p * (Ma - fs) : 0.f);
-    float c1 = wave_sum(lane < NV ? p * Mp : 0.f);
     if (lane < NV) s.vec[lane] = p;
     wsync();
+    float Mp = matvec_lds<NV>(Mrow, s.vec);
+    float c0 = wave_sum(lane < NV ? p * (Ma - fs) : 0.f);
+    float c1 = wave_sum(lane < NV ? p * Mp : 0.f);
 #pragma unroll
     for (int h = 0; h < NRL; h++) {
       int r = lane + 64 * h;
@@ -928,6 +1011,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
     }
     col = a;
   };
+#ifdef AW_NS_SETUP_OLD
   // pairs with K = jd . xd >= MINVAL, in row order: the first NPL get a lane (constants there, xd
   // to the transpose buffer), the rest keep their constants in lane p - NPL
   int npr = 0;
@@ -952,6 +1036,8 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
     }
   }
   const int npl = npr < NPL ? npr : NPL;
+  float jq[NV];
+  (void)jq;
   wsync();
   // pair lanes: the dof columns of their row, xd_q, from the transpose buffer
   if (lane >= NV && lane < NV + npl) {
@@ -966,6 +1052,101 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
     }
   }
   wsync();
+#else
+  // candidate pairs: first rows e of opposing pyramid-edge pairs, in row order, found by a ballot
+  // over the dense rows (no serial scan).  The first NPL get a lane: xd = inv(M) jd' goes to the
+  // transpose buffer here, and the pair lane forms its own constants below (K = jd . xd and
+  // jd . qacc in-lane, no wave reductions on the scan).  A pair with K < MINVAL keeps its lane but
+  // is inert (ca = cb = 0: its update is exactly zero).  Pairs past NPL keep their constants in
+  // lane p - NPL.
+  unsigned long long cmask[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int e = lane + 64 * h;
+    bool c = e + 1 < ndense;
+    if (c) c = s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1;
+    cmask[h] = __ballot(c);
+  }
+  int npr = 0;
+  int ex_e = 0;
+  float ex_ca = 0.f, ex_cb = 0.f, ex_K = 0.f, ex_fa = 0.f, ex_fb = 0.f;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    unsigned long long mk = cmask[h];
+    while (mk) {
+      const int e = 64 * h + __builtin_ctzll(mk);
+      mk &= mk - 1ull;
+      float jd, xd;
+      pair_col(e, jd, xd);
+      const int p = npr++;
+      if (p < NPL) {
+        if (lane < NV) Xb[p * XS + lane] = xd;
+        if (lane == NV + p) rowe = e;
+      } else {
+        const float K = wave_sum(jd * xd);
+        const bool ok = K >= MINVAL;
+        const float ik = ok ? 1.0f / K : 0.f;
+        const float ard = s.efc_aref[nsparse + e] - s.efc_aref[nsparse + e + 1];
+        if (lane == p - NPL) {
+          ex_e = e; ex_ca = ik; ex_cb = ard * ik; ex_K = ok ? K : 0.f;
+          ex_fa = s.efc_force[nsparse + e];
+          ex_fb = s.efc_force[nsparse + e + 1];
+        }
+      }
+    }
+  }
+  const int npl = npr < NPL ? npr : NPL;
+  if (lane < NV) s.rowbuf[lane] = R;   // qacc for the pair lanes' jd . qacc (rowbuf is rewritten after noslip)
+  wsync();
+  const bool pl = lane >= NV && lane < NV + npl;
+  // pair lanes: the dof columns of their row, xd_q, from the transpose buffer
+  if (pl) {
+    const float* xr = Xb + (lane - NV) * XS;
+#pragma unroll
+    for (int q = 0; q < XS / 4; q++) {
+      const float4 v = *reinterpret_cast<const float4*>(xr + 4 * q);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+        if (4 * q + t < NV) Am[4 * q + t] = vv[t];
+    }
+  }
+  // pair lanes: their difference row jd_q (registers), K = jd_q . xd_q, jd_q . qacc and constants
+  float jq[NV];
+  {
+    const int e = pl ? rowe : 0;
+    if (e + 1 < JL) {
+#pragma unroll
+      for (int d = 0; d < NV; d++) jq[d] = s.J[e][d] - s.J[e + 1][d];
+    } else {
+      auto jat = [&](int r, int d) { return r < JL ? s.J[r][d] : jspill_row(m, s, r)[d]; };
+#pragma unroll
+      for (int d = 0; d < NV; d++) jq[d] = jat(e, d) - jat(e + 1, d);
+    }
+    float K = 0.f, S = 0.f;
+#pragma unroll
+    for (int q = 0; q < XS / 4; q++) {
+      const float4 v = *reinterpret_cast<const float4*>(s.rowbuf + 4 * q);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+        if (4 * q + t < NV) {
+          K = fmaf(jq[4 * q + t], Am[4 * q + t], K);
+          S = fmaf(jq[4 * q + t], vv[t], S);
+        }
+    }
+    if (pl) {
+      const bool ok = K >= MINVAL;
+      ca = ok ? 1.0f / K : 0.f;
+      cb = (s.efc_aref[nsparse + e] - s.efc_aref[nsparse + e + 1]) * ca;
+      diag = ok ? K : 0.f;
+      fa = s.efc_force[nsparse + e];
+      fb = s.efc_force[nsparse + e + 1];
+      R = S;
+    }
+  }
+  wsync();
+#endif
   // pair columns of every lane's row: dof lanes read xd_p[lane] back from the transpose buffer;
   // pair lanes form G_q[p] = jd_q . xd_p from their difference row (registers) and xd_p
   // (broadcast reads of the buffer)
@@ -981,7 +1162,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
   }
 #else
   {
-    float jq[NV];
+#ifdef AW_NS_SETUP_OLD
     const int e = lane >= NV && lane < NV + npl ? rowe : 0;
     if (e + 1 < JL) {
 #pragma unroll
@@ -991,6 +1172,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
 #pragma unroll
       for (int d = 0; d < NV; d++) jq[d] = jat(e, d) - jat(e + 1, d);
     }
+#endif
 #pragma unroll
     for (int p = 0; p < NPL; p++) {
       if (p < npl) {
