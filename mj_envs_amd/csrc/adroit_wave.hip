@@ -763,6 +763,10 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
   m.mpr_iterations = (int)B.opt("mpr_iterations", 50);
   m.mpr_tolerance64 = B.opt("mpr_tolerance", 1e-6);
   m.meaninertia = (float)B.opt("meaninertia", 1);
+  // pyramidal cones only: R = max(mjMINVAL, (1 - imp) / imp * diagApprox) per edge row, diagApprox =
+  // invweight_tran + friction^2 * invweight_(tran|rot); impratio (the elliptic cones' friction /
+  // normal impedance ratio) is restated only at its default 1, where it is the identity
+  if (B.opt("impratio", 1) != 1.0) return fail(AW_EUNSUPPORTED, "impratio != 1");
   m.pen_length = (float)B.opt("task_pen_length", 1);
   m.tar_length = (float)B.opt("task_tar_length", 1);
   m.task_kind = B.dim("task_kind"); m.frame_skip = B.dim("task_frame_skip", 1);
