@@ -36,7 +36,11 @@ using namespace aw;
 __device__ unsigned long long g_stage_prof[AW_NPROF];
 #endif
 #ifndef AW_ENV_LANE
-#define AW_ENV_LANE(x) (x)   // -DAW_ENV_LANE=opaque: scratch 272 -> 152 B/lane but -0.3 % (A/B r03i)
+// opaque env-level lane ids: per-lane state / obs addresses are formed where they are used, not
+// once per env and spilled.  With the env index scalar (readfirstlane claim) this takes k_step's
+// scratch 280 -> 92 B/lane and its HBM traffic 7.9 -> 1.7 KB per env-step, +1.7 % (DAPG +2.1 %,
+// A/B r03za); -DAW_ENV_LANE= (plain lane ids) restores the old form.
+#define AW_ENV_LANE(x) opaque(x)
 #endif
 
 // ---------------------------------------------------------------------------------------
@@ -192,7 +196,7 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[Tree<TASK>:
     d.qfrc_con = 0.f;
   } else {
     float a = 0.f;
-    solve_newton<NV>(m, s, lane, Mrow, a, d.qfrc_smooth, d.qacc_smooth);
+    solve_newton<NV, Tree<TASK>::SPLIT>(m, s, lane, Mrow, a, d.qfrc_smooth, d.qacc_smooth);
     AW_PROF(s, PR_NEWTON);
     if (m.noslip_iterations > 0 && !(m.disableflags & DSBL_NOSLIP)) solve_noslip<TASK, KEEP_D>(m, s, lane, Mrow, a);
     AW_PROF(s, PR_NOSLIP);
@@ -441,7 +445,7 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
       }
       store_env<NV>(m, s, st, env, tl);
       AW_PROF(s, PR_TASK);
-      int ended = __shfl(term | trunc, 0, 64);
+      const int ended = __builtin_amdgcn_readfirstlane(term | trunc);
       if (!(autoreset && ended)) break;
       __threadfence_block();
       if (terminal_obs)
@@ -466,7 +470,9 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
     if ((int)gridDim.x >= n) break;            // one env per workgroup: no counter
     int claim = 0;
     if (lane == 0) claim = atomicAdd(next_env, 1);
-    env = (int)gridDim.x + __shfl(claim, 0, 64);
+    // readfirstlane, not a shuffle: env stays a scalar, so the addresses formed from it are
+    // SGPR values instead of per-lane 64-bit VGPR pairs spilled to scratch once per env
+    env = (int)gridDim.x + __builtin_amdgcn_readfirstlane(claim);
   }
 }
 

@@ -393,6 +393,76 @@ AW_DEV void stage_crb(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
   wsync();
   const unsigned long long anc = MD(dof_ancmask, li);
   const float arm = MD(dof_armature, li);
+#ifndef AW_CRB_VALU
+  // P = B C' on the matrix cores (B: rows b_i = crb_{body i} cdof_i, C: rows cdof_k; K = 6 padded
+  // to two K-steps of v_mfma_f32_16x16x4_f32), lower tiles only.  M[i][k] = P[i][k] for k an
+  // ancestor of i and P[k][i] for a descendant, so each lower entry is stored at (i, k) and
+  // (k, i) of a square staging block in the dense-J rows (dead from the narrowphase to the
+  // constraint rows; the pair list / fp64 frames there are consumed) and lane i reads its row
+  // back with 16-byte reads: ~24 LDS ops + 12 MFMAs instead of 33 x (12 broadcast reads + 12 fma).
+  {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    constexpr int NT = (NV + 15) / 16, SS = VS;
+    static_assert(offsetof(Env, rowbuf) == offsetof(Env, J) + sizeof(float) * JL * VS &&
+                  MAXV * SS <= JL * VS + MAXEFC, "CRB staging block does not fit the dense-J rows + rowbuf");
+    float* S = &s.J[0][0];
+    const int sub = lane >> 4, col = lane & 15;
+    f4 acc[NT][NT];
+#pragma unroll
+    for (int ti = 0; ti < NT; ti++)
+#pragma unroll
+      for (int tj = 0; tj <= ti; tj++) acc[ti][tj] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++) {
+      const int c = 4 * ks + sub;
+      const bool cv = c < 6;
+      const int cc = cv ? c : 0;
+      float a[NT], b[NT];
+#pragma unroll
+      for (int t = 0; t < NT; t++) {
+        const int i = 16 * t + col;
+        const bool v = cv && i < NV;
+        const int ii = i < NV ? i : NV - 1;
+        a[t] = v ? s.buf[ii][cc] : 0.f;
+        b[t] = v ? s.cdof[ii][cc] : 0.f;
+      }
+#pragma unroll
+      for (int ti = 0; ti < NT; ti++)
+#pragma unroll
+        for (int tj = 0; tj <= ti; tj++)
+          acc[ti][tj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ti], b[tj], acc[ti][tj], 0, 0, 0);
+    }
+    wsync();
+#pragma unroll
+    for (int ti = 0; ti < NT; ti++)
+#pragma unroll
+      for (int tj = 0; tj <= ti; tj++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int i = 16 * ti + 4 * sub + r, k = 16 * tj + col;
+          if (i < NV && k <= i) {
+            S[i * SS + k] = acc[ti][tj][r];
+            S[k * SS + i] = acc[ti][tj][r];
+          }
+        }
+    wsync();
+    const float* Sr = S + li * SS;
+#pragma unroll
+    for (int q = 0; q < (NV + 3) / 4; q++) {
+      const float4 v4 = *reinterpret_cast<const float4*>(Sr + 4 * q);
+      const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        const int k = 4 * q + t;
+        if (k >= NV) continue;
+        const bool rel = ((anc >> k) & 1ull) || ((MD(dof_ancmask, k) >> li) & 1ull);
+        Mrow[k] = k == li ? vv[t] + arm : (rel ? vv[t] : 0.f);
+      }
+    }
+    wsync();
+    return;
+  }
+#endif
 #pragma unroll
   for (int k = 0; k < NV; k++) {
     float ck[6], bk[6];

@@ -67,6 +67,77 @@ AW_DEV void chol_factor(float (&row)[NV], int lane_in, float& invd, Env& s) {
     }
   }
 }
+// Block-split LDL': when no lower-triangle entry couples the hand block [0, P) with the object
+// block [P, NV) (M is block-diagonal across the dof trees; J'DJ couples them only through a
+// hand-object contact), column j of the hand block and column P + j of the object block are
+// pivoted in the same step, so the serial chain is P columns instead of NV.  Lane i's multiplier
+// is its own entry of its block's current column; updates of a lane's cross-block entries are
+// garbage and are zeroed at the end, updates of an object lane's already-pivoted columns are
+// masked (coefficient 0).  In the decoupled case every operand of the plain factor's fma chain
+// is the same (a cross term enters it as fma(-a, 0, x) = x), so the factor is bitwise the plain
+// one's.
+template <int NV, int P>
+AW_DEV void chol_factor_split(float (&row)[NV], int lane_in, float& invd, Env& s) {
+  constexpr int NB = NV - P, LA = AW_CHOL_LA;
+  static_assert(NB > 0 && NB + LA <= P, "object block must finish before the hand block's look-ahead tail");
+  const int lane = opaque(lane_in);
+  const bool inA = lane < P;
+  float* col = reinterpret_cast<float*>(s.colbuf);
+#pragma unroll
+  for (int j = 0; j < P; j++) {
+    const bool hasB = j < NB;
+    const int jb = hasB ? P + j : P;                 // object column of this step (clamped when done)
+    const float dA = rlane(row[j], j);
+    const float dB = hasB ? rlane(row[jb], jb) : dA;
+    const float dj = __builtin_amdgcn_fmed3f(inA ? dA : dB, MINVAL, 3.402823466e38f);
+    const float inv = __builtin_amdgcn_rcpf(dj);
+    const float a = inA ? row[j] : (hasB ? row[jb] : 0.f);
+    const float aA = inA ? a : 0.f;
+    const int pl = inA ? j : (hasB ? jb : 64);
+    if (lane == pl) invd = inv;
+    const float u = lane > pl ? a * inv : 0.f;
+    if (hasB) {
+      row[j] = inA ? u : row[j];
+      row[jb] = inA ? row[jb] : u;
+    } else {
+      row[j] = u;
+    }
+    // coefficient for column k at this step: an object lane's columns [P, P + j] are pivoted
+    auto coef = [&](int k) { return (k >= P && k <= P + j) ? aA : a; };
+    auto in_la = [&](int k) {
+      return (k > j && k <= j + LA) || (hasB && k > jb && k <= jb + LA);
+    };
+#pragma unroll
+    for (int t = 1; t <= LA; t++) {
+      if (j + t < NV) row[j + t] = fmaf(-coef(j + t), rlane(u, j + t), row[j + t]);
+      if (hasB && jb + t < NV) row[jb + t] = fmaf(-coef(jb + t), rlane(u, jb + t), row[jb + t]);
+    }
+    bool any = false;
+#pragma unroll
+    for (int k = j + 1; k < NV; k++) any = any || !in_la(k);
+    if (any) {
+      col[lane] = u;
+      wsync();
+#pragma unroll
+      for (int q = (j + 1) >> 2; q <= (NV - 1) >> 2; q++) {
+        bool need = false;
+#pragma unroll
+        for (int t = 0; t < 4; t++) need = need || (4 * q + t > j && 4 * q + t < NV && !in_la(4 * q + t));
+        if (!need) continue;
+        const float4 c = s.colbuf[q];
+        const float cv[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+          const int k = 4 * q + t;
+          if (k > j && k < NV && !in_la(k)) row[k] = fmaf(-coef(k), cv[t], row[k]);
+        }
+      }
+      wsync();
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NV; k++) row[k] = (k < P) == inA ? row[k] : 0.f;
+}
 // packed rows of U into s.L (row padding included: the factor-reuse path reloads whole 4-blocks)
 template <int NV>
 AW_DEV void chol_store(const float (&row)[NV], int lane_in, Env& s) {
@@ -623,7 +694,7 @@ AW_DEV void hess_dense_mfma(const DModel& m, Env& s, int lane) {
 }
 #endif
 
-template <int NV>
+template <int NV, int SPLIT = 0>
 AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mrow)[NV], float& a, float qfrc_smooth,
                          float qacc_smooth) {
   const int lane = lane_nt;
@@ -848,6 +919,19 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
 #endif
     wsync();
     AW_PROF(s, PR_NT_HESS);
+#ifdef AW_SPLIT_FACTOR
+    // opt-in: on the A/B the uniform coupling test + the second unrolled factor cost more than the
+    // shorter chain saves (-1.0 % random, -0.4 % DAPG, r03zb; decoupled in most substeps or not,
+    // the code-size growth of +1.4 k instructions lands on the instruction cache)
+    if constexpr (SPLIT > 0 && NV - SPLIT + AW_CHOL_LA <= SPLIT) {
+      // hand / object blocks decoupled (no hand-object contact row in H): the block-split factor
+      bool cpl = false;
+#pragma unroll
+      for (int k = 0; k < SPLIT; k++) cpl = cpl || H[k] != 0.f;
+      if (__ballot(lane >= SPLIT && lane < NV && cpl)) chol_factor<NV>(H, lane, invd, s);
+      else chol_factor_split<NV, SPLIT>(H, lane, invd, s);
+    } else
+#endif
     chol_factor<NV>(H, lane, invd, s);
     chol_store<NV>(H, lane, s);
     wsync();

@@ -44,6 +44,18 @@ template <int TASK> struct Tree {
     return m;
   }
   static constexpr int NLEV = maxdepth() + 1;
+  // first dof of the object block: the smallest p > 0 such that no dof in [p, NV) descends from
+  // a dof in [0, p) (the hand's tree; M is then block-diagonal across p).  0 = no split.
+  static constexpr int split() {
+    for (int p = 1; p < NV; p++) {
+      bool ok = D::parent[p] < 0;
+      for (int j = p; j < NV; j++)
+        if (D::parent[j] >= 0 && D::parent[j] < p) ok = false;
+      if (ok) return p;
+    }
+    return 0;
+  }
+  static constexpr int SPLIT = split();
   static constexpr bool ordered() {   // ancestors before descendants (MuJoCo's dof order)
     for (int j = 0; j < NV; j++)
       if (D::parent[j] >= j) return false;
