@@ -312,7 +312,10 @@ def main():
                     hbm_measured_GBps=round(traffic / (kern_ms * 1e-3) / 1e9, 2) if traffic else None,
                     hbm_measured_frac=round(traffic / (kern_ms * 1e-3) / 1e9 / perfmodel.PEAK_HBM_GBPS, 6)
                     if traffic else None, pmc_source=pmc_src,
-                    note="FP32 roofline (157.3 TFLOP/s: the vector peak, equal to the fp32 MFMA peak the contact Hessian J'DJ runs on); FLOPs "
+                    traffic_bytes_per_env_step=round(traffic / n, 1) if traffic else None,
+                    traffic_over_algorithmic=round(traffic / n / bytes_step, 3) if traffic else None,
+                    note="FP32 roofline (157.3 TFLOP/s: the vector peak, equal to the fp32 MFMA peak the contact Hessian J'DJ, "
+                         "the CRB mass-matrix product and the noslip pair coupling run on); FLOPs "
                          "from perfmodel.py on profiles/work_counts_hammer.json. The HBM figures are far from "
                          "8 TB/s by construction: ~1.1 KB compulsory traffic per env-step (SURVEY 8d), the "
                          "north-star's 40 % of HBM roofline is unreachable on algorithmic bytes")

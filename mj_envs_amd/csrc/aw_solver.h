@@ -1257,9 +1257,89 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
       for (int d = 0; d < NV; d++) jq[d] = jat(e, d) - jat(e + 1, d);
     }
 #endif
+#ifndef AW_NS_G_VALU
+    // G = Jd Xd' (npl x npl, K = NV) on the matrix cores when there are enough pairs: A rows are
+    // the pairs' difference rows jd_q = J_e - J_e+1 read from the Jacobian (LDS rows / global
+    // spill rows; the pair's row index e comes from its lane by a shuffle), B rows the xd_p in
+    // the transpose buffer.  Dof lanes take their xd_p[lane] first; the buffer is then reused to
+    // stage G (row stride 32) and each pair lane reads its row back.
+    bool g_mfma = false;
+    if constexpr (NPL <= 32) {
+      static_assert(32 * 32 * sizeof(float) <= offsetof(Env, qpos), "G staging exceeds the phase-K/S union");
+      if (npl >= 4) {
+        g_mfma = true;
+        typedef float f4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int p = 0; p < NPL; p++)
+          if (p < npl) Ap[p] = Xb[p * XS + li];
+        const int sub = lane >> 4, col = lane & 15;
+        const bool two = npl > 16;
+        const float* r0[2];
+        const float* r1[2];
+        bool qv[2], pv[2];
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+          const int q = 16 * t + col;
+          qv[t] = q < npl;
+          pv[t] = q < npl;
+          // every lane takes part in the shuffle (a lane read while inactive returns nothing)
+          const int es = __shfl(rowe, (NV + q) & 63, 64);
+          const int e = qv[t] ? es : 0;
+          r0[t] = e < JL ? &s.J[e][0] : (const float*)jspill_row(m, s, e);
+          r1[t] = e + 1 < JL ? &s.J[e + 1][0] : (const float*)jspill_row(m, s, e + 1);
+        }
+        f4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c10 = c00, c11 = c00;
+#pragma unroll
+        for (int ks = 0; ks < XS / 4; ks++) {
+          const int k = 4 * ks + sub;
+          const bool kv = k < NV;
+          const int kk = kv ? k : 0;
+          float a[2], b[2];
+#pragma unroll
+          for (int t = 0; t < 2; t++) {
+            a[t] = (kv && qv[t]) ? r0[t][kk] - r1[t][kk] : 0.f;
+            b[t] = (kv && pv[t]) ? Xb[(16 * t + col) * XS + kk] : 0.f;
+          }
+          c00 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c00, 0, 0, 0);
+          if (two) {
+            c01 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[1], c01, 0, 0, 0);
+            c10 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[0], c10, 0, 0, 0);
+            c11 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c11, 0, 0, 0);
+          }
+        }
+        wsync();
+        float* Gb = Xb;   // [32][32]: every operand read above has returned (the MFMAs consumed it)
+        auto put = [&](const f4& c, int ti, int tj) {
+#pragma unroll
+          for (int r = 0; r < 4; r++) Gb[(16 * ti + 4 * sub + r) * 32 + 16 * tj + col] = c[r];
+        };
+        put(c00, 0, 0);
+        if (two) {
+          put(c01, 0, 1);
+          put(c10, 1, 0);
+          put(c11, 1, 1);
+        }
+        wsync();
+        if (pl) {
+          const float* gr = Gb + (lane - NV) * 32;
+#pragma unroll
+          for (int q = 0; q < (NPL + 3) / 4; q++) {
+            const float4 v = *reinterpret_cast<const float4*>(gr + 4 * q);
+            const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+              if (4 * q + t < NPL) Ap[4 * q + t] = vv[t];
+          }
+        }
+        wsync();
+      }
+    }
+#else
+    constexpr bool g_mfma = false;
+#endif
 #pragma unroll
     for (int p = 0; p < NPL; p++) {
-      if (p < npl) {
+      if (p < npl && !g_mfma) {
         const float* xr = Xb + p * XS;
         float g = 0.f;
 #pragma unroll
