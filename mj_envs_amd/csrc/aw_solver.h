@@ -1154,19 +1154,33 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
   int npr = 0;
   int ex_e = 0;
   float ex_ca = 0.f, ex_cb = 0.f, ex_K = 0.f, ex_fa = 0.f, ex_fb = 0.f;
+#ifndef AW_NS_X_VALU
+  // with >= 4 pair lanes the lane pairs' xd = inv(M) jd' come from one MFMA product below
+  // (DAPG +2.7 %, random +-0, r03zg; -DAW_NS_X_VALU keeps the per-pair VALU products)
+  const int npr_all = __popcll(cmask[0]) + __popcll(cmask[1]);
+  // (hammer; relocate's 36 x 36 inv(M) does not fit the staging area, door / pen have 34 pair lanes)
+  constexpr bool X_FIT = NPL <= 32 && NV * XS * sizeof(float) <= offsetof(Env, qpos);
+  const bool x_mfma = X_FIT && (npr_all < NPL ? npr_all : NPL) >= 4;
+#else
+  constexpr bool x_mfma = false;
+#endif
 #pragma unroll
   for (int h = 0; h < 2; h++) {
     unsigned long long mk = cmask[h];
     while (mk) {
       const int e = 64 * h + __builtin_ctzll(mk);
       mk &= mk - 1ull;
-      float jd, xd;
-      pair_col(e, jd, xd);
       const int p = npr++;
       if (p < NPL) {
-        if (lane < NV) Xb[p * XS + lane] = xd;
+        if (!x_mfma) {
+          float jd, xd;
+          pair_col(e, jd, xd);
+          if (lane < NV) Xb[p * XS + lane] = xd;
+        }
         if (lane == NV + p) rowe = e;
       } else {
+        float jd, xd;
+        pair_col(e, jd, xd);
         const float K = wave_sum(jd * xd);
         const bool ok = K >= MINVAL;
         const float ik = ok ? 1.0f / K : 0.f;
@@ -1179,6 +1193,80 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
       }
     }
   }
+#ifndef AW_NS_X_VALU
+  if constexpr (X_FIT) {
+    if (x_mfma) {
+      // X = inv(M) Jd' (NV x npl, K = NV) on the matrix cores: A rows are inv(M)'s rows (each dof
+      // lane stages its row Am in the transpose buffer), B columns the pairs' difference rows
+      // jd_p = J_e - J_e+1 (Jacobian rows in LDS / global spill; e by a shuffle from the pair's
+      // lane); the product is written over the staging as the transpose buffer rows Xb[p][i].
+      typedef float f4 __attribute__((ext_vector_type(4)));
+      constexpr int NTI = (NV + 15) / 16;
+      const int np = npr < NPL ? npr : NPL;
+      if (lane < NV) {
+#pragma unroll
+        for (int q = 0; q < XS / 4; q++) {
+          float4 v;
+          v.x = 4 * q + 0 < NV ? Am[4 * q + 0 < NV ? 4 * q + 0 : 0] : 0.f;
+          v.y = 4 * q + 1 < NV ? Am[4 * q + 1 < NV ? 4 * q + 1 : 0] : 0.f;
+          v.z = 4 * q + 2 < NV ? Am[4 * q + 2 < NV ? 4 * q + 2 : 0] : 0.f;
+          v.w = 4 * q + 3 < NV ? Am[4 * q + 3 < NV ? 4 * q + 3 : 0] : 0.f;
+          *reinterpret_cast<float4*>(Xb + lane * XS + 4 * q) = v;
+        }
+      }
+      wsync();
+      const int sub = lane >> 4, col = lane & 15;
+      const bool two = np > 16;
+      const float* r0[2];
+      const float* r1[2];
+      bool pv[2];
+#pragma unroll
+      for (int t = 0; t < 2; t++) {
+        const int q = 16 * t + col;
+        pv[t] = q < np;
+        const int es = __shfl(rowe, (NV + q) & 63, 64);   // every lane takes part in the shuffle
+        const int e = pv[t] ? es : 0;
+        r0[t] = e < JL ? &s.J[e][0] : (const float*)jspill_row(m, s, e);
+        r1[t] = e + 1 < JL ? &s.J[e + 1][0] : (const float*)jspill_row(m, s, e + 1);
+      }
+      f4 c[NTI][2];
+#pragma unroll
+      for (int ti = 0; ti < NTI; ti++) c[ti][0] = c[ti][1] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < XS / 4; ks++) {
+        const int k = 4 * ks + sub;
+        const bool kv = k < NV;
+        const int kk = kv ? k : 0;
+        float a[NTI], b[2];
+#pragma unroll
+        for (int ti = 0; ti < NTI; ti++) {
+          const int i = 16 * ti + col;
+          a[ti] = (kv && i < NV) ? Xb[(i < NV ? i : 0) * XS + kk] : 0.f;
+        }
+#pragma unroll
+        for (int t = 0; t < 2; t++) b[t] = (kv && pv[t]) ? r0[t][kk] - r1[t][kk] : 0.f;
+#pragma unroll
+        for (int ti = 0; ti < NTI; ti++) {
+          c[ti][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ti], b[0], c[ti][0], 0, 0, 0);
+          if (two) c[ti][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ti], b[1], c[ti][1], 0, 0, 0);
+        }
+      }
+      wsync();
+      // every staged inv(M) operand has returned (the MFMAs consumed it): overwrite with Xb[p][i]
+#pragma unroll
+      for (int ti = 0; ti < NTI; ti++)
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+          if (t == 1 && !two) continue;
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int i = 16 * ti + 4 * sub + r, p = 16 * t + col;
+            if (i < NV) Xb[p * XS + i] = c[ti][t][r];
+          }
+        }
+    }
+  }
+#endif
   const int npl = npr < NPL ? npr : NPL;
   if (lane < NV) s.rowbuf[lane] = R;   // qacc for the pair lanes' jd . qacc (rowbuf is rewritten after noslip)
   wsync();
