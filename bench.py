@@ -4,6 +4,12 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+`--gpus N` outside torch.distributed.run starts N ranks itself (`dist.launch_ranks`: one child
+process per GPU, RANK / LOCAL_RANK / WORLD_SIZE set, the parent never touches the GPU) and exits
+non-zero when fewer than N devices are visible -- it never falls back to one GPU.  `--launch`
+takes the same path at N = 1 (one rank, RCCL process group of one); `--dry-run` runs the launcher
+and the episode-totals exchange over gloo with no GPU and no kernel (the CPU test of this path).
+
 A "step" = one env-step of every env on every GPU: i.i.d. U(-1,1) actions from Philox (seed 0,
 counter (global env id, step)), frame_skip = 5 physics substeps + reward + obs, and auto-reset
 inside the kernel whenever an episode ends.  Episode phases are staggered (each env's first
@@ -79,8 +85,15 @@ def cpu_baseline(blob, env_id, local, budget_s=12.0):
     v, n, steps, dt = run(threads, budget_s * 2 / 3)
     v1, n1, steps1, dt1 = run(1, budget_s / 3)
     return dict(value=round(v, 1), unit="env-steps/s", cores=threads, kind="port",
+                label="restated CPU reference (fp64 C++ oracle of the task layer + MuJoCo 2.1 mj_step)",
                 single_core_value=round(v1, 1), nproc=os.cpu_count(), affinity_cpus=aff,
                 omp_num_threads=os.environ.get("OMP_NUM_THREADS"),
+                all_affinity_cpus_linear_estimate=round(v / threads * aff, 1),
+                why_not_all_cpus=(f"the GPU box grants one GPU's job {threads} host threads (OMP_NUM_THREADS="
+                                  f"{os.environ.get('OMP_NUM_THREADS')}; worker pools must stay within that "
+                                  f"share) while its affinity mask shows all {aff} CPUs of the shared node; "
+                                  f"all_affinity_cpus_linear_estimate scales the measured per-thread rate to "
+                                  f"{aff} CPUs (an upper bound, not measured)") if aff > threads else None,
                 sample=f"{env_id}, the GPU run's first {n} envs (its Philox reset params and actions) x {steps} "
                        f"env-steps on {threads} threads in {dt:.1f} s, and {n1} envs x {steps1} env-steps on 1 "
                        f"thread in {dt1:.1f} s; fp64 C++ oracle (restated mj_step + task layer at MuJoCo's "
@@ -147,21 +160,64 @@ def config2(blob, env_id, device, n=4096, steps=100, warmup=10):
                 ms_per_step=round(dt / steps * 1e3, 4))
 
 
-def pmc_traffic(env_per_launch):
-    """HBM bytes per k_step launch from the latest committed rocprofv3 --pmc summary, or None."""
+def pmc_traffic(envs, env_id, policy, build_id):
+    """HBM bytes per k_step launch (and the summary's FETCH calibration) from the newest committed
+    rocprofv3 --pmc summary whose run matches this one exactly -- env count, task, policy and the
+    kernel build id (hash of the HIP sources + flags) -- or (None, None, None): a summary of another
+    workload or another kernel revision is never reported as this run's traffic."""
     import glob
-    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_kstep.json")))
-    if not paths:
-        return None, None
-    path = paths[-1]
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        if d.get("envs") != env_per_launch:
-            return None, None
-        return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO)
-    except Exception:
-        return None, None
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_kstep.json")), reverse=True)
+    for path in paths:
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if (d.get("envs"), d.get("env_id"), d.get("policy"), d.get("kernel_build_id")) == \
+                (envs, env_id, policy, build_id):
+            return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO), d.get("calibration")
+    return None, None, None
+
+
+def dry_run(args, shard):
+    """The launcher's CPU rehearsal: each rank joins a gloo group, fills its block of the packed
+    episode-totals buffer with rank-specific values (env i of the global batch finished i % 3
+    episodes with return i each, successes on odd global ids) and does the one all-gather bench.py
+    does every horizon; rank 0 prints one JSON line with every rank's shard and the exchange."""
+    import torch
+    import torch.distributed as dist
+    from mj_envs_amd.dist import EpisodeTotals, under_launcher
+    if under_launcher():
+        dist.init_process_group("gloo")
+    n, off = shard.envs_per_rank, shard.env_offset
+    totals = EpisodeTotals(n, shard.world, "cpu")
+    ep, ret, suc = totals.rows()
+    gid = torch.arange(off, off + n)
+    ep.copy_(gid % 3)
+    ret.copy_((gid % 3).float() * gid.float())
+    suc.copy_((gid % 3) * (gid % 2))
+    e, r, s = totals()
+    me = dict(rank=shard.rank, local_rank=shard.local_rank, world=shard.world, env_offset=off, envs=n,
+              pid=os.getpid())
+    ranks = [None] * shard.world
+    if dist.is_initialized():
+        dist.all_gather_object(ranks, me)
+    else:
+        ranks = [me]
+    if shard.rank == 0:
+        gexp = torch.arange(shard.world * n)
+        line = dict(dry_run=True, n_gpus=shard.world, ranks=ranks,
+                    config=dict(parallelism=f"env-shard x{shard.world}", envs_per_gpu=n, total_envs=shard.total_envs),
+                    exchange=dict(backend=dist.get_backend() if dist.is_initialized() else "local copy",
+                                  calls=totals.calls, bytes_per_rank_per_call=totals.bytes_per_rank,
+                                  episodes_ok=bool(torch.equal(e.long(), gexp % 3)),
+                                  returns_ok=bool(torch.equal(r, ((gexp % 3) * gexp).float())),
+                                  successes_ok=bool(torch.equal(s.long(), (gexp % 3) * (gexp % 2))),
+                                  summary=totals.summary()))
+        print(json.dumps(line), flush=True)
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def main():
@@ -186,14 +242,28 @@ def main():
                          "(sampled), or the reference's pretrained DAPG policy (mean action)")
     ap.add_argument("--depth", action="store_true",
                     help="BASELINE config 5: + 64x64 depth-camera obs every env-step (default 8192 envs)")
+    ap.add_argument("--launch", action="store_true",
+                    help="start the ranks through the launcher even for --gpus 1 (one-rank RCCL group)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher + episode-totals exchange over gloo, no GPU, no kernel (CPU test)")
     args = ap.parse_args()
 
-    import numpy as np
-    import torch
-    import torch.distributed as dist
-    from mj_envs_amd import _native, perfmodel
-    from mj_envs_amd.dist import EpisodeTotals, shard_from_env, stagger_phases
-    from mj_envs_amd.tasks import attach_task, load_model
+    from mj_envs_amd.dist import EpisodeTotals, launch_ranks, shard_from_env, stagger_phases, under_launcher
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if under_launcher():
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}")
+    elif args.gpus > 1 or args.launch or args.dry_run:
+        # parent: count devices (no HIP context is created by device_count on this image) and start
+        # one child per GPU; this process never initialises the GPU and never execs
+        if not args.dry_run:
+            import torch
+            have = torch.cuda.device_count()
+            if have < args.gpus:
+                raise SystemExit(f"bench.py --gpus {args.gpus}: only {have} GPU(s) visible; refusing to run "
+                                 f"on fewer ranks")
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], os.path.abspath(__file__)))
 
     if args.depth and args.envs_per_gpu == 65536:
         args.envs_per_gpu = 8192
@@ -203,12 +273,22 @@ def main():
             raise SystemExit("--total-envs must divide evenly over the ranks")
         args.envs_per_gpu = args.total_envs // w
     shard = shard_from_env(args.envs_per_gpu)
+    if args.dry_run:
+        return dry_run(args, shard)
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from mj_envs_amd import _native, perfmodel
+    from mj_envs_amd.tasks import attach_task, load_model
+
     world, rank, local = shard.world, shard.rank, shard.local_rank
-    if world > 1:
-        torch.cuda.set_device(local)
+    if local >= torch.cuda.device_count():
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {torch.cuda.device_count()} GPU(s) visible")
+    torch.cuda.set_device(local)
+    if under_launcher():       # every launched rank, world 1 included, exchanges through RCCL
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
 
     env_id = args.env
     m = attach_task(load_model(env_id), env_id)
@@ -220,11 +300,9 @@ def main():
     rew = sim.empty(n)
     done = sim.empty(n, dtype=torch.uint8)
     goal = sim.empty(n, dtype=torch.uint8)
-    tot_ep = sim.empty(n, dtype=torch.int32)
-    tot_ret = sim.empty(n)
-    tot_suc = sim.empty(n, dtype=torch.int32)
     sticky = sim.empty(n, dtype=torch.int32)
     totals = EpisodeTotals(n, world, dev)
+    tot_ep, tot_ret, tot_suc = totals.rows()          # the kernel writes the send block in place
     sim.reset(obs, seed=SEED_RESET)
     sim.set_episode(ep_len=torch.from_numpy(stagger_phases(n, shard.env_offset, sim.horizon)).to(dev))
     pol = None
@@ -243,7 +321,7 @@ def main():
 
     def gather():
         sim.episode_totals(tot_ep, tot_ret, tot_suc)
-        return totals(tot_ep, tot_ret, tot_suc)      # RCCL all-gather over xGMI when world > 1
+        return totals()          # one RCCL all-gather of the packed [3, E] block when launched
 
     def one_step(k, ev=None):
         if pol is not None:
@@ -271,7 +349,8 @@ def main():
     e0, r0, s0 = (x.clone() for x in gather())
     sim.clear_status()
     torch.cuda.synchronize()
-    if world > 1:
+    pg = dist.is_initialized()
+    if pg:
         dist.barrier()
     events = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in range(args.steps)]
     torch.cuda.synchronize()
@@ -279,18 +358,28 @@ def main():
     for k in range(args.steps):
         one_step(preroll + args.warmup + k, events[k])
     torch.cuda.synchronize()
-    if world > 1:
+    if pg:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern = [e[0].elapsed_time(e[1]) for e in events]
     kern_ms = sum(kern) / args.steps
     depth_ms = sum(e[2].elapsed_time(e[3]) for e in events) / args.steps if depth is not None else None
     e1, r1, s1 = gather()
+    # the exchange's own check: the gathered global totals equal the sum of every rank's block
+    local = torch.stack([tot_ep.long().sum(), tot_suc.long().sum()])
+    if pg:
+        dist.all_reduce(local, op=dist.ReduceOp.SUM)
+    exchange = dict(backend=dist.get_backend() if pg else "local copy", world=world, collective="all_gather_into_tensor"
+                    if pg else None, calls=totals.calls, bytes_per_rank_per_call=totals.bytes_per_rank,
+                    every_steps=sim.horizon, global_episodes=int(e1.long().sum()),
+                    global_successes=int(s1.long().sum()),
+                    gathered_equals_rank_sums=bool(int(e1.long().sum()) == int(local[0])
+                                                   and int(s1.long().sum()) == int(local[1])))
     sim.status(sticky=sticky)
     n_over = int(((sticky & _native.ST_OVERFLOW) != 0).sum())
     n_nan = int(((sticky & (_native.ST_BADQPOS | _native.ST_BADQVEL | _native.ST_BADQACC)) != 0).sum())
     t = torch.tensor([elapsed, kern_ms, n_over, n_nan], dtype=torch.float64, device=dev)
-    if world > 1:
+    if pg:
         dist.all_reduce(t[:2], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[2:], op=dist.ReduceOp.SUM)
     elapsed, kern_ms, n_over, n_nan = float(t[0]), float(t[1]), int(t[2]), int(t[3])
@@ -300,18 +389,25 @@ def main():
         total_steps = world * n * args.steps
         value = total_steps / elapsed
         flops, counts = perfmodel.step_flops(env_id, m, sim.frame_skip)
+        flops_dense, _ = perfmodel.step_flops(env_id, m, sim.frame_skip, dense_m=True)
         achieved = flops * n / (kern_ms * 1e-3) / 1e12
         bytes_step = perfmodel.step_bytes(sim.nq, sim.nv, sim.nu, sim.obs_dim, sim.nparam)
-        traffic, pmc_src = pmc_traffic(n)
+        build_id = _native.kernel_build_id()
+        traffic, pmc_src, pmc_cal = pmc_traffic(n, env_id, args.policy, build_id)
         roof = dict(bound="valu", achieved=round(achieved, 3), peak=perfmodel.PEAK_FP32_TFLOPS,
                     unit="TFLOP/s", frac=round(achieved / perfmodel.PEAK_FP32_TFLOPS, 5), traffic=traffic,
-                    kernel=f"k_step<{sim.nv}>", kernel_ms=round(kern_ms, 4),
+                    kernel=f"k_step<{sim.task_kind}>", nv=sim.nv, kernel_ms=round(kern_ms, 4),
                     kernel_ms_min_max=[round(min(kern), 4), round(max(kern), 4)],
                     flops_per_env_step=round(flops), bytes_per_env_step=bytes_step,
+                    flops_formula="MuJoCo 2.1's algorithms: tree-sparse mj_factorM / mj_solveM for M, dense "
+                                  "Cholesky only for the Newton Hessian (perfmodel.py)",
+                    r03_dense_formula=dict(flops_per_env_step=round(flops_dense),
+                                           frac=round(flops_dense * n / (kern_ms * 1e-3) / 1e12
+                                                      / perfmodel.PEAK_FP32_TFLOPS, 5)),
                     hbm_algorithmic_GBps=round(bytes_step * n / (kern_ms * 1e-3) / 1e9, 2),
                     hbm_measured_GBps=round(traffic / (kern_ms * 1e-3) / 1e9, 2) if traffic else None,
                     hbm_measured_frac=round(traffic / (kern_ms * 1e-3) / 1e9 / perfmodel.PEAK_HBM_GBPS, 6)
-                    if traffic else None, pmc_source=pmc_src,
+                    if traffic else None, pmc_source=pmc_src, pmc_calibration=pmc_cal, kernel_build_id=build_id,
                     traffic_bytes_per_env_step=round(traffic / n, 1) if traffic else None,
                     traffic_over_algorithmic=round(traffic / n / bytes_step, 3) if traffic else None,
                     note="FP32 roofline (157.3 TFLOP/s: the vector peak, equal to the fp32 MFMA peak the contact Hessian J'DJ, "
@@ -347,10 +443,11 @@ def main():
                     dtype="f32",
                     data="synthetic (Philox U(-1,1) actions, reference reset distribution)",
                     config=dict(workload=workload, envs_per_gpu=n, total_envs=world * n,
-                                frame_skip=sim.frame_skip, parallelism=f"env-shard x{world}", preroll=preroll),
+                                frame_skip=sim.frame_skip, parallelism=f"env-shard x{world}", preroll=preroll,
+                                env_id=env_id, policy=args.policy),
                     roofline=roof, finite=finite, overflow_envs=n_over, bad_state_envs=n_nan,
                     capacities=dict(maxcon=sim.maxcon, maxefc=sim.maxefc, maxdense=sim.maxdense),
-                    episodes=episodes)
+                    episodes=episodes, exchange=exchange)
         if world == 1 and not args.no_parity:
             try:
                 line["parity_one_step"] = same_run_parity(blob, sim)
@@ -365,7 +462,7 @@ def main():
             except Exception as e:  # the baseline must not hide the GPU number
                 line["cpu_baseline"] = dict(value=None, error=str(e))
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if pg:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -126,6 +126,26 @@ def stage_profile(reset: bool = True) -> dict:
     return out
 
 
+def kernel_build_id() -> str:
+    """Short hash of the HIP sources, the C-ABI header and the compile flags the product library
+    is built from: ties a committed rocprof summary to the kernel revision it measured."""
+    import hashlib
+    import sys
+    root = os.path.dirname(HERE)
+    h = hashlib.sha256()
+    for d in (os.path.join(HERE, "csrc"), os.path.join(root, "include")):
+        for f in sorted(os.listdir(d)):
+            with open(os.path.join(d, f), "rb") as fh:
+                h.update(f.encode() + b"\0" + fh.read())
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    import __graft_entry__
+    h.update(" ".join(__graft_entry__.HIPCC_FLAGS).encode())
+    if os.environ.get("AW_LIB"):
+        h.update(os.path.basename(os.environ["AW_LIB"]).encode())
+    return h.hexdigest()[:12]
+
+
 def _check(rc: int):
     if rc != 0:
         raise NativeError(f"adroit_wave error {rc}: {load().aw_last_error().decode()}")

@@ -5,12 +5,20 @@ Philox stream (reset draws, random actions, policy noise) by the GLOBAL env id
 (``aw_set_env_offset``), so a run on N GPUs reproduces the one-GPU run of the same global batch
 bit for bit.  The only collective is the episode bookkeeping exchange the reference's drivers do
 on the host: every rank contributes its block's per-env totals over finished episodes (count,
-summed return, successes) and all ranks receive the global vectors (RCCL all-gather over xGMI on
-MI355X; gloo in the CPU tests).
+summed return, successes) and all ranks receive the global vectors -- ONE all-gather of a packed
+[3, E] int32 block per exchange (RCCL over xGMI on MI355X; gloo in the CPU tests).
+
+The reference never parallelised its drivers (``mj_envs_vision/run.py:48``: "TODO: create worker
+setup and parallelise"); ``launch_ranks`` is the one-process-per-GPU launcher ``bench.py --gpus N``
+uses when it is not already running under ``torch.distributed.run``.
 """
 from __future__ import annotations
 
 import os
+import socket
+import subprocess
+import sys
+import time
 from dataclasses import dataclass
 
 
@@ -36,6 +44,11 @@ def shard_from_env(envs_per_rank: int) -> Shard:
                  local_rank=int(os.environ.get("LOCAL_RANK", "0")), envs_per_rank=envs_per_rank)
 
 
+def under_launcher() -> bool:
+    """True inside a rank started by torch.distributed.run or by ``launch_ranks``."""
+    return "WORLD_SIZE" in os.environ and "RANK" in os.environ
+
+
 def stagger_phases(n: int, env_offset: int, horizon: int, seed: int = 0x5A66):
     """Per-env starting step of the first episode, a hash of the global env id modulo the horizon
     (independent of the sharding): envs then reach their horizon -- and auto-reset -- on
@@ -49,31 +62,102 @@ def stagger_phases(n: int, env_offset: int, horizon: int, seed: int = 0x5A66):
 
 
 class EpisodeTotals:
-    """Preallocated all-gather of the per-env totals over finished episodes
-    (``aw_episode_totals``): every finished episode is counted exactly once, whenever it ended."""
+    """Preallocated exchange of the per-env totals over finished episodes (``aw_episode_totals``):
+    every finished episode is counted exactly once, whenever it ended.
 
-    def __init__(self, envs_per_rank: int, world: int, device, group=None):
+    The send block is one int32 [3, E] tensor -- row 0 episode counts, row 1 the fp32 bits of the
+    summed returns, row 2 successes -- whose rows ``rows()`` hands to the kernel as three contiguous
+    vectors, so a rank's contribution is written in place and leaves in ONE all-gather of 12 E
+    bytes per horizon (768 KiB per rank at 65 536 envs; SURVEY §5 sizes the exchange).  With
+    no process group (a single process) the exchange is a local copy."""
+
+    def __init__(self, envs_per_rank: int, world: int, device, group=None, collective: bool | None = None):
         import torch
-        self.world = world
-        self.group = group
-        self.episodes = torch.zeros(world * envs_per_rank, dtype=torch.int32, device=device)
-        self.sum_return = torch.zeros(world * envs_per_rank, dtype=torch.float32, device=device)
-        self.successes = torch.zeros(world * envs_per_rank, dtype=torch.int32, device=device)
-
-    def __call__(self, episodes, sum_return, successes):
         import torch.distributed as dist
-        if self.world == 1:
-            self.episodes.copy_(episodes)
-            self.sum_return.copy_(sum_return)
-            self.successes.copy_(successes)
+        self.world = world
+        self.envs = envs_per_rank
+        self.group = group
+        self.collective = (dist.is_available() and dist.is_initialized()) if collective is None else collective
+        if world > 1 and not self.collective:
+            raise RuntimeError("EpisodeTotals: world > 1 needs an initialised process group")
+        self.send = torch.zeros(3, envs_per_rank, dtype=torch.int32, device=device)
+        self.recv = torch.zeros(world, 3, envs_per_rank, dtype=torch.int32, device=device)
+        self.calls = 0
+
+    def rows(self):
+        """(episodes int32, sum_return float32, successes int32) views of the send block."""
+        import torch
+        return self.send[0], self.send[1].view(torch.float32), self.send[2]
+
+    @property
+    def bytes_per_rank(self) -> int:
+        return self.send.numel() * self.send.element_size()
+
+    def __call__(self, episodes=None, sum_return=None, successes=None):
+        """Exchange (optionally copying the given per-env vectors into the send block first) and
+        return the global (episodes, sum_return, successes) vectors in global env order."""
+        import torch
+        import torch.distributed as dist
+        e, r, s = self.rows()
+        for dst, src in ((e, episodes), (r, sum_return), (s, successes)):
+            if src is not None and src.data_ptr() != dst.data_ptr():
+                dst.copy_(src)
+        if self.collective:
+            dist.all_gather_into_tensor(self.recv.view(-1), self.send.view(-1), group=self.group)
         else:
-            dist.all_gather_into_tensor(self.episodes, episodes, group=self.group)
-            dist.all_gather_into_tensor(self.sum_return, sum_return, group=self.group)
-            dist.all_gather_into_tensor(self.successes, successes, group=self.group)
-        return self.episodes, self.sum_return, self.successes
+            self.recv[0].copy_(self.send)
+        self.calls += 1
+        g = self.recv.transpose(0, 1)                     # [3, world, E]
+        return (g[0].reshape(-1), g[1].reshape(-1).view(torch.float32), g[2].reshape(-1))
 
     def summary(self) -> dict:
         """global episode count, mean return per finished episode, success rate (%)"""
-        n = int(self.episodes.sum())
-        return dict(episodes=n, mean_return=float(self.sum_return.double().sum()) / max(n, 1),
-                    success_pct=100.0 * int(self.successes.sum()) / max(n, 1))
+        import torch
+        e, r, s = self.recv[:, 0], self.recv[:, 1].contiguous().view(torch.float32), self.recv[:, 2]
+        n = int(e.sum())
+        return dict(episodes=n, mean_return=float(r.double().sum()) / max(n, 1),
+                    success_pct=100.0 * int(s.sum()) / max(n, 1))
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(nproc: int, argv: list[str], script: str, env_extra: dict | None = None,
+                 poll_s: float = 0.2) -> int:
+    """Start ``nproc`` ranks of ``script`` (one process per GPU, ranks 0..nproc-1 on local devices
+    0..nproc-1) with torch.distributed.run's environment contract (RANK, LOCAL_RANK, WORLD_SIZE,
+    LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT) and wait for them.  The caller must not
+    have touched the GPU (the ranks are children, never an exec of this process).  If a rank
+    fails, the others are terminated (by their own handles) and its exit code is returned."""
+    port = free_port()
+    procs = []
+    for r in range(nproc):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc),
+                   LOCAL_WORLD_SIZE=str(nproc), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), **(env_extra or {}))
+        procs.append(subprocess.Popen([sys.executable, script, *argv], env=env))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in live:
+                        q.terminate()
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc if rc >= 0 else 128 - rc

@@ -106,13 +106,25 @@ class AdroitVecEnv:
         self.sim.random_actions(out, seed, step)
         return out
 
+    def mj_viewer_headless_setup(self, width: Optional[int] = None, height: Optional[int] = None,
+                                 aerial: bool = False):
+        """``headless_observer.py:20-31`` (+ ``set_view``, ``:59-66``): the offscreen free camera
+        (azimuth 90, distance 4.5, elevation from the observed body; ``aerial`` flips the
+        elevation's sign as ``set_view('aerial')`` / pen's ``use_aerial_view`` do).  Here it builds
+        the camera record every env of the batch is rendered from (``render.free_camera``) and
+        returns it; ``render_depth`` uses it from then on."""
+        from .render import free_camera
+        w, h = (width or self._cam_key[0], height or self._cam_key[1]) if getattr(self, "_cam_key", None) \
+            else (width or 64, height or 64)
+        self._aerial = bool(aerial)
+        self._cam, self._cam_key = free_camera(self.model, self.env_id, w, h, aerial=self._aerial), (w, h)
+        return self._cam
+
     def render_depth(self, width: int = 64, height: int = 64, out=None):
         """Depth frames [N, height, width] (metres, device) of every env's current state from
         the reference's headless camera (headless_observer.py; mj_envs_amd/render.py)."""
-        from .render import free_camera
-        key = (width, height)
-        if getattr(self, "_cam_key", None) != key:
-            self._cam, self._cam_key = free_camera(self.model, self.env_id, width, height), key
+        if getattr(self, "_cam_key", None) != (width, height):
+            self.mj_viewer_headless_setup(width, height, aerial=getattr(self, "_aerial", False))
         if out is None:
             out = self.sim.empty(self.num_envs, height, width)
         self.sim.render_depth(out, self._cam)
@@ -186,6 +198,7 @@ class _AdroitEnv(_reference_base()):
         self.render_mode, self.width, self.height = render_mode, width, height
         self.is_headless = is_headless
         self.variation_type = variation_type
+        self.observer = None            # the camera record once mj_viewer_headless_setup() ran
         self.vec = AdroitVecEnv(self.env_id, 1, device=device, variation_type=variation_type,
                                 seed=1, autoreset=False)
         self.model = self.vec.model
@@ -271,6 +284,50 @@ class _AdroitEnv(_reference_base()):
         returns an RGB frame from OpenGL (headless_observer.py:34-52); RGB is not rendered here,
         the HIP ray caster produces metric depth from the same camera (mj_envs_amd/render.py)."""
         return self.vec.render_depth(self.width, self.height)[0].cpu().numpy().astype(np.float64)
+
+    # pen's flag (pen_v0.py:23, read by its mj_viewer_headless_setup, :174-177)
+    use_aerial_view = False
+
+    def mj_viewer_headless_setup(self):
+        """The reference's offscreen camera setup, called by ``record_policy``
+        (``utils/visualize_env.py:115``) and by door / pen / relocate on every reset
+        (``hammer_v0.py:161-165``, ``door_v0.py:146``, ``pen_v0.py:160-177``, ``relocate_v0.py:138``):
+        builds the free camera of ``render.free_camera`` for this env's frame size (pen: from its
+        'target' body, with ``use_aerial_view`` flipping the elevation).  Returns the camera record."""
+        self.observer = self.vec.mj_viewer_headless_setup(
+            self.width, self.height, aerial=self.env_id == "pen-v0" and bool(self.use_aerial_view))
+        return self.observer
+
+    # --- mjrl MujocoEnv members (inherited when mjrl is importable; mujoco-py is never created) ---
+    @property
+    def dt(self) -> float:
+        """mjrl ``MujocoEnv.dt``: model timestep x frame_skip."""
+        return float(self.model.opt["timestep"]) * self.frame_skip
+
+    def state_vector(self):
+        """mjrl ``MujocoEnv.state_vector``: concatenated qpos, qvel (fp64)."""
+        qp, qv = self._qpos_qvel()
+        return np.concatenate([qp, qv])
+
+    def set_state(self, qpos, qvel):
+        """mjrl ``MujocoEnv.set_state``: qpos / qvel with the current model parameters, then a
+        forward pass (the next ``get_obs`` reflects the new state)."""
+        self._set(qpos, qvel, self._params())
+
+    def do_simulation(self, ctrl, n_frames):
+        raise NotImplementedError(
+            "do_simulation: the HIP step kernel runs frame_skip substeps of the task's own action "
+            "scaling inside step(a); raw-ctrl stepping through mujoco-py is not part of the drop-in")
+
+    def mj_viewer_setup(self):
+        raise NotImplementedError("mj_viewer_setup: on-screen (GLFW) viewing is out of scope; use "
+                                  "mj_viewer_headless_setup() + render()")
+
+    def viewer_setup(self):
+        raise NotImplementedError("viewer_setup: on-screen viewing is out of scope")
+
+    def mj_render(self):
+        raise NotImplementedError("mj_render: on-screen viewing is out of scope; use render()")
 
     def close(self):
         self.vec.close()

@@ -52,8 +52,10 @@ def _geom_world0(model):
     return xpos, gpos
 
 
-def free_camera(model, env_id: str, width: int = 64, height: int = 64, zfar: float = ZFAR) -> np.ndarray:
-    """The reference's headless camera as the ``AW_CAM_FLOATS`` record of ``aw_render_depth``.
+def free_camera(model, env_id: str, width: int = 64, height: int = 64, zfar: float = ZFAR,
+                aerial: bool = False) -> np.ndarray:
+    """The reference's headless camera as the ``AW_CAM_FLOATS`` record of ``aw_render_depth``
+    (``aerial``: ``set_view('aerial')``, elevation -45 - deg(...)/2, ``headless_observer.py:62-63``).
 
     Layout: position[3], forward[3], up[3], right[3], u0, du, v0, dv, zfar.  A ray through output
     pixel (row i, col j) has direction forward + (u0 + du*j) * right + (v0 - dv*i) * up.
@@ -69,7 +71,7 @@ def free_camera(model, env_id: str, width: int = 64, height: int = 64, zfar: flo
         bid = model.name2id("body", bid)
     v = xpos[bid] - cam_world
     ratio = float(np.clip(v[0] / v[2], -1.0, 1.0)) if v[2] != 0 else 0.0
-    elevation = -45.0 + math.degrees(math.acos(ratio)) / 2.0
+    elevation = -45.0 + (-1.0 if aerial else 1.0) * math.degrees(math.acos(ratio)) / 2.0
     azimuth, distance = 90.0, 4.5
     az, el = math.radians(azimuth), math.radians(elevation)
     fwd = np.array([math.cos(el) * math.cos(az), math.cos(el) * math.sin(az), math.sin(el)])

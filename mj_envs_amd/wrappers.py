@@ -38,12 +38,20 @@ STATE_KEY = "state"
 
 
 class PixelObservationVecEnv:
-    """``CustomPixelObservationWrapper`` over an ``AdroitVecEnv`` (device tensors)."""
+    """``CustomPixelObservationWrapper`` over an ``AdroitVecEnv`` (device tensors), or over a
+    single-env facade (``HammerEnvV0`` ...; its batch of one is wrapped).  ``host_tensors=True``
+    returns CPU float tensors and takes numpy / CPU actions, as the reference wrapper does
+    (``wrappers.py:55,70-76``), so the reference's drivers -- ``record_policy``
+    (``utils/visualize_env.py:108-128``): ``gym_env.env.mj_viewer_headless_setup()``,
+    ``reset``, ``get_pixels().numpy()``, ``step(gym_env, a)`` -- run unchanged."""
 
     def __init__(self, env: AdroitVecEnv, obs_key: str = PIXELS_KEY, render_kwargs: Optional[dict] = None,
-                 action_repeat: int = 1):
+                 action_repeat: int = 1, host_tensors: bool = False):
         if obs_key not in (PIXELS_KEY, STATE_KEY):
             raise KeyError(obs_key)
+        if not isinstance(env, AdroitVecEnv) and isinstance(getattr(env, "vec", None), AdroitVecEnv):
+            env = env.vec                     # a single-env facade: wrap its batch of one
+        self.host_tensors = bool(host_tensors)
         rk = render_kwargs or {}
         self.env = env
         self.num_envs = env.num_envs
@@ -61,8 +69,11 @@ class PixelObservationVecEnv:
         self.observation_space = self.pixel_space if obs_key == PIXELS_KEY else self.state_space
 
     # --- observations --------------------------------------------------------------------
+    def _out(self, t):
+        return t.cpu().clone() if self.host_tensors else t
+
     def get_state(self):
-        return self.env.obs
+        return self._out(self.env.obs)
 
     def get_pixels(self):
         if not self._pixels_fresh:
@@ -71,10 +82,22 @@ class PixelObservationVecEnv:
             self.env.render_depth(self.width, self.height, out=self._pixels.view(self.num_envs, self.height,
                                                                                  self.width))
             self._pixels_fresh = True
-        return self._pixels
+        return self._out(self._pixels)
 
     def _obs(self):
         return self.get_pixels() if self.obs_key == PIXELS_KEY else self.get_state()
+
+    def mj_viewer_headless_setup(self):
+        """forwarded to the env, as gym's wrapper attribute lookup does for the reference"""
+        return self.env.mj_viewer_headless_setup(self.width, self.height)
+
+    def _actions(self, actions):
+        import torch
+        if isinstance(actions, torch.Tensor) and actions.device == self.env.sim.torch_device:
+            return actions
+        a = torch.as_tensor(np.asarray(actions, np.float32) if not isinstance(actions, torch.Tensor)
+                            else actions.float())
+        return a.reshape(self.num_envs, -1).to(self.env.sim.torch_device)
 
     # --- episode control -----------------------------------------------------------------
     def reset(self, **kw):
@@ -84,6 +107,7 @@ class PixelObservationVecEnv:
         return self._obs(), {}
 
     def step(self, actions):
+        actions = self._actions(actions)
         obs, rew, term, trunc, info = self.env.step(actions)
         self._pixels_fresh = False
         reward = rew.clone()
@@ -106,6 +130,9 @@ class PixelObservationVecEnv:
             info["goal_achieved"] = self.env.goal.bool()
         ended = term | trunc
         self.timer.masked_fill_(ended, 0)       # the kernel auto-reset these envs
+        if self.host_tensors:
+            reward, term, trunc = reward.cpu(), term.cpu(), trunc.cpu()
+            info = {k: (v.cpu() if hasattr(v, "cpu") else v) for k, v in info.items()}
         return self._obs(), reward, term, trunc, info
 
     def close(self):

@@ -75,3 +75,91 @@ def test_stagger_phases_cover_horizon():
     assert ph.min() == 0 and ph.max() == 199
     counts = np.bincount(ph, minlength=200)
     assert counts.min() > 0.8 * 65536 / 200 and counts.max() < 1.2 * 65536 / 200
+
+
+# --- bench.py's own launcher: `--gpus N` starts N ranks itself -----------------
+import json
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*argv, timeout=180):
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *argv], capture_output=True,
+                          text=True, timeout=timeout, env=env, cwd=REPO)
+
+
+def test_bench_launcher_dry_run_world2():
+    """--gpus 2 outside torchrun: two child ranks (distinct pids), env offsets 0 and E, world 2,
+    and the packed [3, E] exchange delivers every rank's block in global env order."""
+    E = 16
+    p = _bench("--gpus", "2", "--dry-run", "--envs-per-gpu", str(E))
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1                                   # rank 0 prints the one line
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "env-shard x2"
+    ranks = sorted(d["ranks"], key=lambda r: r["rank"])
+    assert [(r["rank"], r["local_rank"], r["world"], r["env_offset"]) for r in ranks] == [(0, 0, 2, 0), (1, 1, 2, E)]
+    assert ranks[0]["pid"] != ranks[1]["pid"] and os.getpid() not in (ranks[0]["pid"], ranks[1]["pid"])
+    x = d["exchange"]
+    assert x["backend"] == "gloo" and x["calls"] == 1 and x["bytes_per_rank_per_call"] == 3 * 4 * E
+    assert x["episodes_ok"] and x["returns_ok"] and x["successes_ok"]
+    g = np.arange(2 * E)
+    assert x["summary"]["episodes"] == int((g % 3).sum())
+
+
+def test_bench_launcher_refuses_missing_gpus():
+    """Never a silent fall-back to fewer ranks: with fewer visible GPUs than --gpus it exits non-zero."""
+    import torch
+    n = max(2, torch.cuda.device_count() + 1)
+    p = _bench("--gpus", str(n), "--steps", "1", "--warmup", "0", "--envs-per-gpu", "8")
+    assert p.returncode != 0
+    assert "refusing" in (p.stdout + p.stderr)
+
+
+def test_launch_ranks_propagates_failure(tmp_path):
+    """A failing rank's exit code is the launcher's; the other ranks are stopped."""
+    from mj_envs_amd.dist import launch_ranks
+    script = tmp_path / "rank.py"
+    script.write_text("import os, sys, time\n"
+                      "r = int(os.environ['RANK'])\n"
+                      "assert os.environ['WORLD_SIZE'] == '3' and os.environ['MASTER_ADDR'] == '127.0.0.1'\n"
+                      "if r == 1: sys.exit(3)\n"
+                      "time.sleep(60)\n")
+    import time
+    t0 = time.time()
+    assert launch_ranks(3, [], str(script)) == 3
+    assert time.time() - t0 < 30
+
+
+def test_bench_world_mismatch_refused():
+    env = dict(os.environ, RANK="0", WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="1")
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "4", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=REPO)
+    assert p.returncode != 0 and "WORLD_SIZE" in p.stderr
+
+
+@pytest.mark.gpu
+def test_bench_launcher_one_gpu_rccl():
+    """`bench.py --gpus 1 --launch` through the same launcher code the N-GPU run uses: one child
+    rank, an RCCL process group of one, the packed episode-totals all-gather every horizon."""
+    p = _bench("--gpus", "1", "--launch", "--steps", "20", "--warmup", "2", "--preroll", "200",
+               "--envs-per-gpu", "4096", "--no-cpu-baseline", "--no-parity", "--no-config2", timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    print(json.dumps(dict(value=d["value"], exchange=d["exchange"], episodes=d["episodes"])))
+    assert d["n_gpus"] == 1 and d["config"]["parallelism"] == "env-shard x1"
+    assert d["config"]["total_envs"] == 4096 and d["value"] > 0 and d["finite"]
+    x = d["exchange"]
+    assert x["backend"] == "nccl" and x["collective"] == "all_gather_into_tensor" and x["world"] == 1
+    assert x["calls"] == 3 and x["bytes_per_rank_per_call"] == 3 * 4 * 4096
+    assert x["gathered_equals_rank_sums"]
+    assert x["global_episodes"] >= 4096                   # every env ended >= 1 episode in the pre-roll
+    assert 0 < d["episodes"]["finished_in_timed_window"] <= 4096

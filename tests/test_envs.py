@@ -188,11 +188,30 @@ def test_facades_derive_from_mjrl_mujocoenv(tmp_path):
     pkg.mkdir(parents=True)
     (tmp_path / "mjrl" / "__init__.py").write_text("")
     (pkg / "__init__.py").write_text("")
-    (pkg / "mujoco_env.py").write_text("class MujocoEnv:\n    def __init__(self, *a, **k):\n        raise RuntimeError('mujoco-py')\n")
+    # the stand-in carries the MujocoEnv members that read mujoco-py state (self.sim / self.model.opt)
+    (pkg / "mujoco_env.py").write_text(
+        "class MujocoEnv:\n"
+        "    def __init__(self, *a, **k):\n        raise RuntimeError('mujoco-py')\n"
+        "    @property\n    def dt(self):\n        return self.model.opt.timestep * self.frame_skip\n"
+        "    def state_vector(self):\n        return self.sim.data.qpos\n"
+        "    def set_state(self, qpos, qvel):\n        self.sim.set_state(qpos)\n"
+        "    def do_simulation(self, ctrl, n_frames):\n        self.sim.step()\n"
+        "    def mj_viewer_setup(self):\n        self.viewer = None\n")
     code = ("import mjrl.envs.mujoco_env as M\n"
             "from mj_envs_amd import envs\n"
             "for c in (envs.HammerEnvV0, envs.DoorEnvV0, envs.PenEnvV0, envs.RelocateEnvV0):\n"
             "    assert issubclass(c, M.MujocoEnv), c\n"
+            "    for name in ('dt', 'state_vector', 'set_state', 'do_simulation', 'mj_viewer_setup',\n"
+            "                 'mj_viewer_headless_setup'):\n"
+            "        assert getattr(c, name) is envs._AdroitEnv.__dict__[name], (c, name)\n"
+            "        assert getattr(c, name) is not getattr(M.MujocoEnv, name, None), (c, name)\n"
+            "e = object.__new__(envs.HammerEnvV0)\n"
+            "e.frame_skip = 5\n"
+            "e.model = type('Mdl', (), {'opt': {'timestep': 0.002}})()\n"
+            "assert abs(e.dt - 0.01) < 1e-12, e.dt\n"
+            "for call in (lambda: e.do_simulation(None, 5), e.mj_viewer_setup):\n"
+            "    try:\n        call()\n        raise SystemExit('no raise')\n"
+            "    except NotImplementedError:\n        pass\n"
             "print('ok')\n")
     import os
     env = dict(os.environ, PYTHONPATH=os.pathsep.join([str(tmp_path), os.path.dirname(os.path.dirname(os.path.abspath(__file__)))]))
@@ -200,3 +219,65 @@ def test_facades_derive_from_mjrl_mujocoenv(tmp_path):
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr
     from mj_envs_amd import envs
     assert envs._reference_base() is object   # no mjrl in this interpreter
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env_id", ["hammer-v0", "door-v0", "pen-v0", "relocate-v0"])
+def test_record_policy_drives_facade(env_id):
+    """utils/visualize_env.py:108-128 (record_policy) on the drop-in, call for call:
+    gym_env.env.mj_viewer_headless_setup(), reset(gym_env), gym_env.get_pixels().numpy(),
+    policy.act(obs), step(gym_env, action)[:3] -- through PixelObservationVecEnv on the facade."""
+    import mj_envs_amd
+    from mj_envs_amd.render import free_camera
+    from mj_envs_amd.wrappers import PixelObservationVecEnv, reset, step
+    e = mj_envs_amd.make(env_id)
+    gym_env = PixelObservationVecEnv(e, obs_key="pixels", host_tensors=True)
+    cam = gym_env.env.mj_viewer_headless_setup()
+    np.testing.assert_array_equal(cam, free_camera(e.model, env_id, 64, 64))
+    rng = np.random.default_rng(3)
+
+    class RandomPolicy:                       # the reference's policies return a [1, nu] tensor
+        def act(self, obs):
+            return torch.FloatTensor(rng.uniform(-1, 1, (1, e.action_space.shape[0])))
+
+    policy = RandomPolicy()
+    obs, _ = reset(gym_env)
+    trajectory = [gym_env.get_pixels().numpy()]
+    for t in range(4):
+        action = policy.act(obs)
+        obs, reward, term = step(gym_env, action)[:3]
+        trajectory.append(gym_env.get_pixels().numpy())
+        if bool(term.any()):
+            break
+    assert len(trajectory) >= 2
+    for f in trajectory:
+        assert f.shape == (1, 1, 64, 64) and np.isfinite(f).all() and f.min() > 0
+    assert not np.array_equal(trajectory[0], trajectory[-1])        # the hand moved
+    assert obs.device.type == "cpu" and reward.shape == (1,)
+    # the single-env facade itself: headless setup + render from the same camera
+    np.testing.assert_array_equal(e.mj_viewer_headless_setup(), cam)
+    assert e.render().shape == (64, 64)
+    if env_id == "pen-v0":
+        e.use_aerial_view = True
+        assert not np.array_equal(e.mj_viewer_headless_setup(), cam)
+    gym_env.close()
+
+
+@pytest.mark.gpu
+def test_facade_mjrl_members():
+    """mjrl MujocoEnv's dt / state_vector / set_state on the facade."""
+    from mj_envs_amd.envs import HammerEnvV0
+    e = HammerEnvV0()
+    assert e.dt == pytest.approx(0.002 * 5)
+    sv = e.state_vector()
+    assert sv.shape == (e.vec.nq + e.vec.nv,)
+    qp, qv = sv[:e.vec.nq].copy(), sv[e.vec.nq:].copy()
+    qp[0] += 0.05
+    qv[:] = 0.0
+    e.set_state(qp, qv)
+    sv2 = e.state_vector()
+    np.testing.assert_allclose(sv2[:e.vec.nq], qp, atol=1e-6)
+    np.testing.assert_allclose(sv2[e.vec.nq:], 0.0, atol=0)
+    with pytest.raises(NotImplementedError):
+        e.do_simulation(np.zeros(26), 5)
+    e.close()

@@ -32,6 +32,20 @@ def test_camera_record():
         assert np.isclose(c[14] - c[15] * 31.5, 0.0, atol=1e-6)
 
 
+def test_camera_aerial_view():
+    """set_view('aerial') (headless_observer.py:62-63; pen's use_aerial_view, pen_v0.py:174-175):
+    elevation -45 - d/2 instead of -45 + d/2, same azimuth, distance and look-at point."""
+    from mj_envs_amd.render import free_camera
+    from mj_envs_amd.tasks import load_model
+    m = load_model("pen-v0")
+    c0 = free_camera(m, "pen-v0").astype(np.float64)
+    c1 = free_camera(m, "pen-v0", aerial=True).astype(np.float64)
+    el0, el1 = np.degrees(np.arcsin(c0[5])), np.degrees(np.arcsin(c1[5]))
+    assert np.isclose(el0 + el1, -90.0, atol=1e-3) and not np.isclose(el0, el1)
+    look0, look1 = c0[:3] + 4.5 * c0[3:6], c1[:3] + 4.5 * c1[3:6]
+    assert np.allclose(look0, look1, atol=1e-5)
+
+
 def test_checker_analytic():
     """numpy checker on shapes with closed-form depth"""
     from oracle.depth import render_depth

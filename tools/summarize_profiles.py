@@ -27,6 +27,16 @@ def pmc(path, counter, kernel="k_step"):
     return vals, meta
 
 
+def last_json(path):
+    """the last JSON line a bench run printed (None if the file is absent or has none)"""
+    if not os.path.exists(path):
+        return None
+    for ln in reversed(open(path).read().splitlines()):
+        if ln.startswith("{"):
+            return json.loads(ln)
+    return None
+
+
 def main(tag):
     src = os.path.join(REPO, "gpurun_out", tag)
     dst = os.path.join(REPO, "profiles")
@@ -44,12 +54,17 @@ def main(tag):
     # calibration kernel on the same box: k_random_actions writes exactly n*nu*4 bytes
     cal, _ = pmc(os.path.join(src, "pmc_write", "pw_counter_collection.csv"), "WRITE_SIZE", "k_random_actions")
     # persistent k_step workgroups: the grid is the resident-slot count, not the env count
-    envs = b["config"].get("envs_per_gpu", meta["grid"] // meta["wg"])
+    # the run identity comes from the bench line the PMC pass itself printed (falls back to the
+    # pass's bench.json); bench.py's pmc_traffic only reports a summary whose identity matches
+    pb = last_json(os.path.join(src, "pmc_fetch.log")) or b
+    envs = pb["config"].get("envs_per_gpu", meta["grid"] // meta["wg"])
     fetch_b = statistics.mean(fetch) * 1024
     write_b = statistics.mean(write) * 1024
-    nu = 26 if "hammer" in b["config"]["workload"] else None
+    nu = 26 if "hammer" in pb["config"]["workload"] else None
     out = dict(
         tag=tag, kernel=meta["name"], envs=envs, launches=len(fetch),
+        env_id=pb["config"].get("env_id"), policy=pb["config"].get("policy"),
+        kernel_build_id=pb["roofline"].get("kernel_build_id"),
         fetch_size_kb=[round(v, 3) for v in fetch], write_size_kb=[round(v, 3) for v in write],
         fetch_bytes_per_launch=round(fetch_b), write_bytes_per_launch=round(write_b),
         hbm_bytes_per_launch=round(fetch_b + write_b),
