@@ -3,6 +3,12 @@
 // One workgroup = one 64-lane wave = one env.  A step launch runs frame_skip x mj_step
 // (forward + Euler) and the task layer for every env; the per-env working set stays in LDS /
 // VGPRs for the whole launch, so HBM traffic is the compulsory state + action + obs bytes.
+//
+// Build split (__graft_entry__.py): the library is this file compiled five times in parallel and
+// linked -- once per task with -DAW_TASK_TU=<task> (that task's kernels and its launcher table,
+// task_ops<TASK>) and once with -DAW_API_TU (the C-ABI and the task-independent kernels, no
+// per-task instantiation).  A plain compile of the file (diagnostic builds: -DAW_ONLY_TASK,
+// -DAW_STAGE_PROF) is the whole library in one translation unit.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -19,7 +25,9 @@
 #include "aw_common.h"
 #include "aw_dynamics.h"
 #include "aw_render.h"
+#ifndef AW_TASK_TU
 #include "aw_policy.h"
+#endif
 #include "aw_solver.h"
 #include "aw_task.h"
 #include "aw_tree.h"
@@ -33,6 +41,9 @@ using namespace aw;
 #endif
 
 #ifdef AW_STAGE_PROF
+#if defined(AW_TASK_TU) || defined(AW_API_TU)
+#error "the stage profiler counts into one device global: build it as a single translation unit"
+#endif
 __device__ unsigned long long g_stage_prof[AW_NPROF];
 #endif
 #ifndef AW_ENV_LANE
@@ -347,23 +358,14 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
                                              float* terminal_obs, int autoreset, uint64_t seed,
                                              int* __restrict__ next_env) {
   constexpr int NV = Tree<TASK>::NV;
-#ifndef AW_MODEL_BYVAL
   // model scalars read from the device copy on demand (scalar loads behind the loop's memory
   // clobber) instead of ~50 kernel-argument SGPRs held live across the whole launch
   const DModel& m = *mptr;
   (void)mval;
-#else
-  const DModel& m = mval;
-  (void)mptr;
-#endif
-#ifndef AW_STATE_BYVAL
   // the state pointers read from the device header where they are used (the loop's memory
   // clobber forces the reload) instead of ~30 SGPRs of kernel arguments live across the launch
   const DState& st = *reinterpret_cast<const DState*>(mptr + 1);   // DState follows DModel in the header
   (void)stval;
-#else
-  const DState& st = stval;
-#endif
   __shared__ Env s;
   const int lane = threadIdx.x;
   // Persistent workgroups: the grid is one workgroup per resident slot (launch_step); each takes
@@ -395,14 +397,10 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
       // memory clobber: keeps LICM from hoisting the (loop-invariant) model loads of a whole
       // substep out of this loop, which would pin them in registers across every stage
       asm volatile("" ::: "memory");
-#ifndef AW_NO_OPAQUE_LANE
       // and no lane-dependent value is hoisted out of the loop either (the lane id is re-derived
       // per substep): loop-invariant masks and offsets would otherwise occupy SGPRs / VGPRs across
       // every stage of the substep
       const int sl = opaque(lane);
-#else
-      const int sl = lane;
-#endif
       if (!resetting && !retry) check_state<NV>(s, sl);
       AW_PROF(s, PR_CHECK);
       forward<TASK>(m, s, sl, Mrow, d);
@@ -567,6 +565,7 @@ __global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const
   }
 }
 
+#ifndef AW_TASK_TU   // task-independent kernels: in the API translation unit only
 __global__ void __launch_bounds__(64) k_task_eval(DModel m, int n, const float* qpos, const float* qvel,
                                                   const float* xpos, const float* xquat, const float* sxpos,
                                                   const float* touch, float* obs, float* reward, uint8_t* done,
@@ -648,6 +647,8 @@ __global__ void __launch_bounds__(64) k_collide_test(DModel m, int n, const int*
   }
 }
 
+#endif  // AW_TASK_TU
+
 // depth frame of every env's current state: wave 0 runs the kinematics, then all four waves
 // cast the pixels (one workgroup per env; render geom poses staged in LDS)
 struct CamRec {
@@ -673,6 +674,7 @@ __global__ void __launch_bounds__(256) k_depth(DModel m, DState st, int n, CamRe
   for (int p0 = (tid >> 6) * 64; p0 < W * H; p0 += 256) render_span(rg, m.nrgeom, cam.c, W, H, p0, lane, o);
 }
 
+#ifndef AW_TASK_TU
 __global__ void k_random_actions(int n, int nu, uint64_t seed, uint64_t step, uint64_t env_offset, float* out) {
   int env = blockIdx.x * blockDim.x + threadIdx.x;
   if (env >= n) return;
@@ -684,8 +686,11 @@ __global__ void k_random_actions(int n, int nu, uint64_t seed, uint64_t step, ui
   }
 }
 
+#endif  // AW_TASK_TU
+
 // ---------------------------------------------------------------------------------------
 // host side
+#ifndef AW_TASK_TU
 namespace {
 thread_local std::string g_err;
 int fail(int code, const std::string& msg) { g_err = msg; return code; }
@@ -729,6 +734,8 @@ bool put_arr(T (&dst)[N], const std::vector<U>& v) {
 std::vector<float> tof(const std::vector<double>& v) { return std::vector<float>(v.begin(), v.end()); }
 }  // namespace
 
+#endif  // AW_TASK_TU
+
 struct aw_handle {
   int device, nenv, NV;
   DModel m;
@@ -742,6 +749,7 @@ struct aw_handle {
   int grid_env = -1;         // AW_STEP_GRID at create (-1: unset)
 };
 
+#ifndef AW_TASK_TU
 static int upload_header(aw_handle* h) {
   HIPCHK(hipMemcpy(h->dmhdr, &h->m, sizeof(DModel), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy((DModel*)h->dmhdr + 1, &h->st, sizeof(DState), hipMemcpyHostToDevice));
@@ -1059,6 +1067,8 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
   return AW_OK;
 }
 
+#endif  // AW_TASK_TU
+
 // resident k_step workgroups on the handle's device (occupancy x CUs): the persistent grid
 template <int TASK>
 static int step_slots(int device) {
@@ -1095,6 +1105,29 @@ template <int TASK>
 static void launch_depth(aw_handle* h, const CamRec& cam, int W, int H, float* out, hipStream_t st) {
   hipLaunchKernelGGL((k_depth<TASK>), dim3(h->nenv), dim3(256), 0, st, h->m, h->st, h->nenv, cam, W, H, out);
 }
+
+// The launchers of one task, behind one table.  Split build: task_ops<TASK> is defined (and with
+// it every kernel of TASK instantiated) only in the -DAW_TASK_TU=TASK translation unit; the API
+// unit sees the declaration and calls it across the link.
+struct TaskOps {
+  int (*slots)(int device);
+  void (*step)(aw_handle*, const float*, float*, float*, uint8_t*, uint8_t*, float*, int, uint64_t, hipStream_t);
+  void (*reset)(aw_handle*, const uint8_t*, const float*, uint64_t, float*, hipStream_t);
+  void (*set)(aw_handle*, const float*, const float*, const float*, const float*, float*, hipStream_t);
+  void (*dump)(aw_handle*, int, const float*, float*, hipStream_t);
+  void (*depth)(aw_handle*, const CamRec&, int, int, float*, hipStream_t);
+};
+template <int TASK> const TaskOps* task_ops();
+#ifndef AW_API_TU
+template <int TASK> const TaskOps* task_ops() {
+  static const TaskOps ops = {step_slots<TASK>, launch_step<TASK>, launch_reset<TASK>, launch_set<TASK>,
+                              launch_dump<TASK>, launch_depth<TASK>};
+  return &ops;
+}
+#endif
+#ifdef AW_TASK_TU
+template const TaskOps* task_ops<AW_TASK_TU>();
+#else
 
 // kernels are instantiated per task (the dof tree of aw_trees.h is a template argument)
 #ifdef AW_ONLY_TASK
@@ -1143,7 +1176,7 @@ static int update_slots(aw_handle* h) {
     h->slots = h->grid_env > 0 ? h->grid_env : (1 << 30);
     return AW_OK;
   }
-#define CALL(TT) (h->slots = step_slots<TT>(h->device))
+#define CALL(TT) (h->slots = task_ops<TT>()->slots(h->device))
   DISPATCH_TASK(h->m.task_kind, CALL)
 #undef CALL
   return AW_OK;
@@ -1244,7 +1277,7 @@ int aw_set_option(aw_handle* h, int disableflags, int iterations, int noslip_ite
 int aw_reset(aw_handle* h, const uint8_t* mask, const float* params, uint64_t seed, float* obs, void* stream) {
   if (!h) return fail(AW_EINVAL, "aw_reset: null");
   HIPCHK(hipSetDevice(h->device));
-#define CALL(TT) launch_reset<TT>(h, mask, params, seed, obs, (hipStream_t)stream)
+#define CALL(TT) task_ops<TT>()->reset(h, mask, params, seed, obs, (hipStream_t)stream)
   DISPATCH_TASK(h->m.task_kind, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());
@@ -1255,7 +1288,7 @@ int aw_step(aw_handle* h, const float* actions, float* obs, float* reward, uint8
             float* terminal_obs, int autoreset, uint64_t seed, void* stream) {
   if (!h || !actions || !obs || !reward || !done || !goal) return fail(AW_EINVAL, "aw_step: null buffer");
   HIPCHK(hipSetDevice(h->device));
-#define CALL(TT) launch_step<TT>(h, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, (hipStream_t)stream)
+#define CALL(TT) task_ops<TT>()->step(h, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, (hipStream_t)stream)
   DISPATCH_TASK(h->m.task_kind, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());
@@ -1289,7 +1322,7 @@ int aw_set_state(aw_handle* h, const float* qpos, const float* qvel, const float
                  float* obs, void* stream) {
   if (!h) return fail(AW_EINVAL, "aw_set_state: null");
   HIPCHK(hipSetDevice(h->device));
-#define CALL(TT) launch_set<TT>(h, qpos, qvel, warm, params, obs, (hipStream_t)stream)
+#define CALL(TT) task_ops<TT>()->set(h, qpos, qvel, warm, params, obs, (hipStream_t)stream)
   DISPATCH_TASK(h->m.task_kind, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());
@@ -1396,7 +1429,7 @@ int aw_task_eval(aw_handle* h, int n, const float* qpos, const float* qvel, cons
 int aw_forward_dump(aw_handle* h, int env, const float* ctrl, float* out, void* stream) {
   if (!h || !out || env < 0 || env >= h->nenv) return fail(AW_EINVAL, "aw_forward_dump: bad arguments");
   HIPCHK(hipSetDevice(h->device));
-#define CALL(TT) launch_dump<TT>(h, env, ctrl, out, (hipStream_t)stream)
+#define CALL(TT) task_ops<TT>()->dump(h, env, ctrl, out, (hipStream_t)stream)
   DISPATCH_TASK(h->m.task_kind, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());
@@ -1409,7 +1442,7 @@ int aw_render_depth(aw_handle* h, const float* cam, int width, int height, float
   HIPCHK(hipSetDevice(h->device));
   CamRec c;
   memcpy(c.c, cam, sizeof(c.c));   // host array: the camera record travels as a kernel argument
-#define CALL(TT) launch_depth<TT>(h, c, width, height, out, (hipStream_t)stream)
+#define CALL(TT) task_ops<TT>()->depth(h, c, width, height, out, (hipStream_t)stream)
   DISPATCH_TASK(h->m.task_kind, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());
@@ -1457,3 +1490,4 @@ int aw_stage_profile(unsigned long long* out, int reset) {
 }
 
 }  // extern "C"
+#endif  // !AW_TASK_TU

@@ -176,24 +176,13 @@ struct MData {
 #ifndef AW_MD_AS
 #define AW_MD_AS 4
 #endif
-#ifndef AW_MD_FLAT
 template <class T>
 AW_DEV T mld(const T* base, unsigned i) {
   typedef const __attribute__((address_space(AW_MD_AS))) T GT;
   typedef const __attribute__((address_space(AW_MD_AS))) char GC;
   return *(GT*)((GC*)base + i * (unsigned)sizeof(T));
 }
-#else
-template <class T>
-AW_DEV T mld(const T* base, unsigned i) {
-  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + i * (unsigned)sizeof(T));
-}
-#endif
-#ifndef AW_MD_INLINE_LOC
 #define MD(name, idx) ::aw::mld(m.d->name, (unsigned)(idx))
-#else   // analysis builds (tools/isa_regions.py): the load is attributed to the reading line
-#define MD(name, idx) (*(const __attribute__((address_space(1))) __typeof__(m.d->name[0])*)((const __attribute__((address_space(1))) char*)(m.d->name) + (unsigned)(idx) * (unsigned)sizeof(m.d->name[0])))
-#endif
 // device-global views of model / state arrays (global_load / global_store, not flat)
 template <class T> using gp_t = __attribute__((address_space(1))) T*;
 template <class T> AW_DEV gp_t<const T> gcp(const T* p) { return (gp_t<const T>)p; }

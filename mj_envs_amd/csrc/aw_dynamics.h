@@ -53,7 +53,6 @@ AW_DEV void stage_kinematics(const DModel& m, Env& s, int lane) {
     s.xquat[0][0] = 1; s.xquat[0][1] = s.xquat[0][2] = s.xquat[0][3] = 0;
   }
   wsync();
-#ifndef AW_KIN_LEVEL
   // Body frames without a level sweep.  (A) Lane b composes its body offset and its joints into
   // ONE rigid transform T_b in the parent's frame -- every lane at once, nothing read from another
   // lane -- and leaves its joints' axes / anchors in that frame.  (B) Global frames by pointer
@@ -83,7 +82,7 @@ AW_DEV void stage_kinematics(const DModel& m, Env& s, int lane) {
         add3(xn, xn, tp);
         copy3(s.xaxis[j], xa);    // parent frame; (C) makes them global
         copy3(s.xanchor[j], xn);
-        // hardware v_sin / v_cos on the half angle reduced to [-pi, pi] (see AW_KIN_LEVEL below)
+        // hardware v_sin / v_cos on the half angle reduced to [-pi, pi]
         const float hq = hinge ? 0.5f * q : 0.f;
         const float hr = fmaf(-6.28318530717958648f, rintf(hq * 0.159154943091895336f), hq);
         const float sn = __sinf(hr), cs = __cosf(hr);
@@ -141,69 +140,6 @@ AW_DEV void stage_kinematics(const DModel& m, Env& s, int lane) {
     }
     wsync();
   }
-#else
-  // lane b owns body b (nbody <= 64) and works at its tree level; its model data (and its first
-  // joint's) are loaded once before the level sweep, so a level costs LDS reads of the parent
-  // frame + arithmetic, not a chain of dependent model loads
-  const bool own = lane > 0 && lane < m.nbody;
-  const int b = own ? lane : 0;
-  const int dep = own ? MD(body_depth, b) : -1;
-  const int p = MD(body_parentid, b), da = MD(body_dofadr, b), dn = own ? MD(body_dofnum, b) : 0;
-  float bp[3], bq[4], ax0[3], jp0[3];
-  for (int k = 0; k < 3; k++) bp[k] = MD(body_pos, 3 * b + k);
-  for (int k = 0; k < 4; k++) bq[k] = MD(body_quat, 4 * b + k);
-  if (own && MD(body_ovr, b)) { apply_ovr<3>(m, s, 0, b, bp); apply_ovr<4>(m, s, 1, b, bq); }
-  const int j0 = dn > 0 ? da : 0;
-  for (int q = 0; q < 3; q++) { ax0[q] = MD(jnt_axis, 3 * j0 + q); jp0[q] = MD(jnt_pos, 3 * j0 + q); }
-  const int jt0 = MD(jnt_type, j0);
-  for (int lev = 1; lev < m.nlevel; lev++) {
-    if (dep == lev) {
-      float xp[3], xq[4], pq[4];
-      for (int k = 0; k < 4; k++) pq[k] = s.xquat[p][k];
-      rotvq(xp, bp, pq);
-      add3(xp, xp, s.xpos[p]);
-      mulq(xq, pq, bq);
-      for (int k = 0; k < dn; k++) {
-        const int j = da + k;
-        float axis[3], xaxis[3], xanchor[3], jp[3];
-        int jt = jt0;
-        if (k == 0) {
-          for (int q = 0; q < 3; q++) { axis[q] = ax0[q]; jp[q] = jp0[q]; }
-        } else {
-          for (int q = 0; q < 3; q++) { axis[q] = MD(jnt_axis, 3 * j + q); jp[q] = MD(jnt_pos, 3 * j + q); }
-          jt = MD(jnt_type, j);
-        }
-        rotvq(xaxis, axis, xq);
-        rotvq(xanchor, jp, xq);
-        add3(xanchor, xanchor, xp);
-        float q = s.qpos[j];
-        if (jt == JNT_SLIDE) {
-          for (int c = 0; c < 3; c++) xp[c] += xaxis[c] * q;
-        } else {
-          float sn, cs, ql[4], v[3];
-          // hardware v_sin / v_cos (the library sinf / cosf pair was ~80 VALU per hinge on the
-          // level sweep's critical path).  Their absolute error grows with |x|, and the object
-          // hinges (OBJRx/y/z) are unlimited, so the half angle is first reduced to [-pi, pi]:
-          // q/2 - 2 pi round(q / (4 pi)), exact enough for any reachable angle.
-          const float hq = 0.5f * q;
-          const float hr = fmaf(-6.28318530717958648f, rintf(hq * 0.159154943091895336f), hq);
-          sn = __sinf(hr);
-          cs = __cosf(hr);
-          ql[0] = cs; ql[1] = axis[0] * sn; ql[2] = axis[1] * sn; ql[3] = axis[2] * sn;
-          mulq(xq, xq, ql);
-          rotvq(v, jp, xq);
-          sub3(xp, xanchor, v);
-        }
-        copy3(s.xaxis[j], xaxis);
-        copy3(s.xanchor[j], xanchor);
-      }
-      normq(xq);
-      copy3(s.xpos[b], xp);
-      for (int c = 0; c < 4; c++) s.xquat[b][c] = xq[c];
-    }
-    wsync();
-  }
-#endif
   // geoms (compact collidable list), sites, inertial frames
   for (int g = lane; g < m.ngeom; g += 64) {
     int b = MD(geom_bodyid, g);
@@ -393,7 +329,6 @@ AW_DEV void stage_crb(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
   wsync();
   const unsigned long long anc = MD(dof_ancmask, li);
   const float arm = MD(dof_armature, li);
-#ifndef AW_CRB_VALU
   // P = B C' on the matrix cores (B: rows b_i = crb_{body i} cdof_i, C: rows cdof_k; K = 6 padded
   // to two K-steps of v_mfma_f32_16x16x4_f32), lower tiles only.  M[i][k] = P[i][k] for k an
   // ancestor of i and P[k][i] for a descendant, so each lower entry is stored at (i, k) and
@@ -462,7 +397,6 @@ AW_DEV void stage_crb(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
     wsync();
     return;
   }
-#endif
 #pragma unroll
   for (int k = 0; k < NV; k++) {
     float ck[6], bk[6];
@@ -487,7 +421,6 @@ AW_DEV float stage_velocity(const DModel& m, Env& s, int lane) {
     if (!(m.disableflags & DSBL_GRAVITY)) { cacc[0][3] = -m.gravity[0]; cacc[0][4] = -m.gravity[1]; cacc[0][5] = -m.gravity[2]; }
   }
   wsync();
-#ifndef AW_RNE_LEVEL
   // cvel / cacc as tree prefix sums (pointer jumping, log2(depth) rounds) of per-body local terms:
   // cvel_b = cvel_parent + sum_j cdof_j qvel_j; cacc_b = cacc_parent + sum_j (cv_j x cdof_j) qvel_j
   // with cv_j the velocity before joint j (mj_comVel's per-joint order inside the body)
@@ -541,30 +474,6 @@ AW_DEV float stage_velocity(const DModel& m, Env& s, int lane) {
       }
     tree_prefix(cacc, la);
   }
-#else
-  {
-    // lane b owns body b at its tree level (as in stage_kinematics)
-    const bool own = lane > 0 && lane < m.nbody;
-    const int b = own ? lane : 0;
-    const int dep = own ? MD(body_depth, b) : -1;
-    const int p = MD(body_parentid, b), da = MD(body_dofadr, b), dn = own ? MD(body_dofnum, b) : 0;
-    for (int lev = 1; lev < m.nlevel; lev++) {
-      if (dep == lev) {
-        float cv[6], ca[6];
-        for (int k = 0; k < 6; k++) { cv[k] = cvel[p][k]; ca[k] = cacc[p][k]; }
-        for (int q = 0; q < dn; q++) {
-          int j = da + q;
-          float cd[6], cdd[6], qv = s.qvel[j];
-          for (int k = 0; k < 6; k++) cd[k] = s.cdof[j][k];
-          cross_motion(cdd, cv, cd);
-          for (int k = 0; k < 6; k++) { cv[k] += cd[k] * qv; ca[k] += cdd[k] * qv; }
-        }
-        for (int k = 0; k < 6; k++) { cvel[b][k] = cv[k]; cacc[b][k] = ca[k]; }
-      }
-      wsync();
-    }
-  }
-#endif
   // local body force: cinert*cacc + cvel x* (cinert*cvel), written over cacc
   for (int b = 1 + lane; b < m.nbody; b += 64) {
     float f[6], t1[6], t2[6];

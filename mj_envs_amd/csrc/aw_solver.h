@@ -27,7 +27,6 @@ namespace aw {
 #ifndef AW_CHOL_LA
 #define AW_CHOL_LA 2
 #endif
-#ifndef AW_CHOL_LLT
 // LDL' (default): H = U D U' with U unit lower triangular, right-looking with look-ahead.  Column
 // j: pivot D_j = H'_jj (clamped at MINVAL like mju_cholFactor's diagonal), U_ij = H'_ij / D_j; the
 // rank-1 update H'_ik -= H'_ij U_kj takes the lane's own unscaled entry and the published scaled
@@ -163,122 +162,6 @@ AW_DEV float chol_solve(const float (&row)[NV], float invd, float b, int lane_in
   }
   return lane < NV ? b : 0.f;
 }
-#else
-#ifdef AW_CHOL_READLANE
-// Variant: the column is broadcast with v_readlane (SGPR operands) instead of an LDS round trip.
-template <int NV>
-AW_DEV void chol_factor(float (&row)[NV], int lane_in, float& invd, Env& s) {
-  const int lane = opaque(lane_in);   // lane compares are made here, not hoisted out of the caller's loop
-#pragma unroll
-  for (int j = 0; j < NV; j++) {
-    const float djj = __builtin_amdgcn_fmed3f(rlane(row[j], j), MINVAL, 3.402823466e38f);   // max(d, MINVAL) without the canonicalising v_max
-    const float inv = __builtin_amdgcn_rsqf(djj);
-    const float sq = djj * inv;
-    row[j] = lane == j ? sq : row[j] * inv;
-    if (lane == j) invd = inv;
-    const float lij = row[j];
-#pragma unroll
-    for (int k = j + 1; k < NV; k++) row[k] = fmaf(-lij, rlane(lij, k), row[k]);
-  }
-}
-#elif AW_CHOL_LA > 0
-// Look-ahead (default; -DAW_CHOL_LA=0 selects the plain form below): column j's entries for the
-// next AW_CHOL_LA pivot rows (j+1 .. j+LA) travel by v_readlane (SGPR broadcast) and update those
-// rows at once, so pivot j+1 waits only on this column's readlane, not on the LDS round trip; the
-// rest of the rank-1 update (rows > j+LA) reads the column from LDS and lags behind the pivot
-// chain.  Same operands in every fma: bitwise the plain form's factor (A/B -0.35 %, r03d).
-template <int NV>
-AW_DEV void chol_factor(float (&row)[NV], int lane_in, float& invd, Env& s) {
-  const int lane = opaque(lane_in);   // lane compares are made here, not hoisted out of the caller's loop
-  constexpr int LA = AW_CHOL_LA;
-  float* col = reinterpret_cast<float*>(s.colbuf);
-#pragma unroll
-  for (int j = 0; j < NV; j++) {
-    const float djj = __builtin_amdgcn_fmed3f(rlane(row[j], j), MINVAL, 3.402823466e38f);   // max(d, MINVAL) without the canonicalising v_max
-    const float inv = __builtin_amdgcn_rsqf(djj);
-    const float sq = djj * inv;
-    row[j] = lane == j ? sq : row[j] * inv;
-    if (lane == j) invd = inv;
-    const float lij = row[j];
-#pragma unroll
-    for (int a = 1; a <= LA; a++)
-      if (j + a < NV) row[j + a] = fmaf(-lij, rlane(lij, j + a), row[j + a]);
-    if (j + LA + 1 < NV) {
-      col[lane] = lij;
-      wsync();
-#pragma unroll
-      for (int q = (j + LA + 1) >> 2; q <= (NV - 1) >> 2; q++) {
-        const float4 c = s.colbuf[q];
-        const float cv[4] = {c.x, c.y, c.z, c.w};
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-          const int k = 4 * q + t;
-          if (k > j + LA && k < NV) row[k] = fmaf(-lij, cv[t], row[k]);
-        }
-      }
-      wsync();
-    }
-  }
-}
-#else
-template <int NV>
-AW_DEV void chol_factor(float (&row)[NV], int lane_in, float& invd, Env& s) {
-  const int lane = opaque(lane_in);   // lane compares are made here, not hoisted out of the caller's loop
-  float* col = reinterpret_cast<float*>(s.colbuf);
-#pragma unroll
-  for (int j = 0; j < NV; j++) {
-    const float djj = __builtin_amdgcn_fmed3f(rlane(row[j], j), MINVAL, 3.402823466e38f);   // max(d, MINVAL) without the canonicalising v_max
-    const float inv = __builtin_amdgcn_rsqf(djj);   // v_rsq_f32: one op on the column's critical path
-    const float sq = djj * inv;
-    row[j] = lane == j ? sq : row[j] * inv;
-    if (lane == j) invd = inv;
-    if (j + 1 < NV) {
-      col[lane] = row[j];
-      wsync();
-      const float lij = row[j];
-#pragma unroll
-      for (int q = (j + 1) >> 2; q <= (NV - 1) >> 2; q++) {
-        const float4 c = s.colbuf[q];
-        const float cv[4] = {c.x, c.y, c.z, c.w};
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-          const int k = 4 * q + t;
-          if (k > j && k < NV) row[k] = fmaf(-lij, cv[t], row[k]);
-        }
-      }
-      wsync();
-    }
-  }
-}
-#endif
-template <int NV>
-AW_DEV void chol_store(const float (&row)[NV], int lane_in, Env& s) {
-  const int lane = opaque(lane_in);
-  if (lane < NV) {
-#pragma unroll
-    for (int k = 0; k < NV; k++)
-      if (k <= lane) s.L[tri(lane) + k] = row[k];
-  }
-}
-// x = inv(L L') b, b lane-distributed; L rows in registers (forward) and packed in LDS (backward)
-template <int NV>
-AW_DEV float chol_solve(const float (&row)[NV], float invd, float b, int lane_in, const Env& s) {
-  const int lane = opaque(lane_in);
-#pragma unroll
-  for (int j = 0; j < NV; j++) {
-    float yj = rlane(b, j) * rlane(invd, j);
-    if (lane == j) b = yj;
-    else if (lane > j) b = fmaf(-row[j], yj, b);
-  }
-#pragma unroll
-  for (int j = NV - 1; j >= 0; j--) {
-    float xj = rlane(b, j) * rlane(invd, j);
-    if (lane == j) b = xj;
-    else if (lane < j) b = fmaf(-s.L[tri(j) + lane], xj, b);
-  }
-  return lane < NV ? b : 0.f;
-}
-#endif   // AW_CHOL_LLT
 // y = M x with M lane-distributed rows and x in LDS (broadcast reads)
 template <int NV>
 AW_DEV float matvec_lds(const float (&row)[NV], const float* x) {
@@ -627,10 +510,9 @@ AW_DEV float row_eval(const RowR& r, float jar, float* force, int* st) {
   *force = 0.f; *st = S_SAT; return 0.f;
 }
 
-#ifndef AW_HESS_VALU
 // J_d' diag(w) J_d over the dense rows (weights w_d in s.rowbuf[nsparse + d], 0 for rows outside
-// the quadratic zone) on the matrix cores, written into the packed lower triangle s.L (default;
-// -DAW_HESS_VALU: rank-1 VALU updates per row).  v_mfma_f32_16x16x4_f32 takes four rows per
+// the quadratic zone) on the matrix cores, written into the packed lower triangle s.L (the
+// rank-1 VALU updates per row are in git history, r03p).  v_mfma_f32_16x16x4_f32 takes four rows per
 // K-step: lane l supplies A[i = l&15][k = l>>4] = w_d J[d][16 ti + i] and B[k][j = l&15] =
 // J[d][16 tj + j] with d = d0 + (l>>4); accumulator register r of lane l is entry
 // (16 ti + 4 (l>>4) + r, 16 tj + (l&15)).  Tiles (0,0), (1,0), (1,1) cover rows < 32 and, for
@@ -641,6 +523,8 @@ AW_DEV float row_eval(const RowR& r, float jar, float* force, int* st) {
 template <int NV>
 AW_DEV void hess_dense_mfma(const DModel& m, Env& s, int lane) {
   typedef float f4 __attribute__((ext_vector_type(4)));
+  // three row tiles: rows 32.. come from the third tile's b2 = Jr[32 + (col & 3)] (4 columns)
+  static_assert(NV <= 36, "hess_dense_mfma covers at most 36 dofs");
   constexpr bool X2 = NV > 32;
   const int nd = s.ndense, ns = s.nsparse;
   const int sub = lane >> 4, col = lane & 15;
@@ -692,7 +576,6 @@ AW_DEV void hess_dense_mfma(const DModel& m, Env& s, int lane) {
     put(c22, 2, 2);
   }
 }
-#endif
 
 template <int NV, int SPLIT = 0>
 AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mrow)[NV], float& a, float qfrc_smooth,
@@ -788,51 +671,6 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
       }
     }
     if (full) {
-#ifdef AW_HESS_REGOFFD
-    // Hessian H = M + J' D_quad J.  Sparse rows: diagonal terms gathered through an LDS vector,
-    // the off-diagonal term of a two-dof (tendon) row added in registers by the two lanes it
-    // couples; dense rows: rank-1 updates with the row broadcast from LDS.
-    if (lane < NV) s.hdiag[lane] = 0.f;
-    wsync();
-    unsigned long long offd[NRL];
-#pragma unroll
-    for (int h = 0; h < NRL; h++) {
-      int r = lane + 64 * h;
-      bool od = false;
-      if (r < nefc) {
-        float w = rr[h].st == S_QUAD ? rr[h].D : 0.f;
-        s.rowbuf[r] = w;
-        if (r < s.nsparse && w != 0.f) {
-          int i0 = s.efc_i0[r], i1 = s.efc_i1[r];
-          float v0 = s.efc_v0[r], v1 = s.efc_v1[r];
-          atomicAdd(&s.hdiag[i0], w * v0 * v0);
-          if (i1 >= 0) { atomicAdd(&s.hdiag[i1], w * v1 * v1); od = true; }
-        }
-      }
-      offd[h] = __ballot(od);
-    }
-    wsync();
-    AW_PROF(s, PR_NT_HSPARSE);
-    {
-      const float dg = s.hdiag[li];
-#pragma unroll
-      for (int k = 0; k < NV; k++) H[k] = Mrow[k] + (k == lane ? dg : 0.f);
-    }
-#pragma unroll
-    for (int h = 0; h < NRL; h++) {
-      while (offd[h]) {
-        const int r = 64 * h + __builtin_ctzll(offd[h]);
-        offd[h] &= offd[h] - 1ull;
-        const int i0 = __builtin_amdgcn_readfirstlane(s.efc_i0[r]);
-        const int i1 = __builtin_amdgcn_readfirstlane(s.efc_i1[r]);
-        const float val = s.rowbuf[r] * s.efc_v0[r] * s.efc_v1[r];
-        const int other = lane == i0 ? i1 : (lane == i1 ? i0 : -1);
-#pragma unroll
-        for (int k = 0; k < NV; k++) H[k] += k == other ? val : 0.f;
-        AW_PROF_ADD(s, PR_NT_OFFD_ROWS, 1);
-      }
-    }
-#else
     // Hessian H = M + J' D_quad J, lower triangle only (the right-looking factorisation never
     // reads a lane's entries above its diagonal).  Sparse rows (<= 2 dofs: frictionloss, joint
     // and tendon limits) are scattered with LDS atomics into the packed lower triangle in the
@@ -840,7 +678,6 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
     // with 16-byte reads -- a two-dof tendon row's off-diagonal term lands in ONE entry, where
     // adding it in registers took a 2 x NV select chain per row.  Dense rows: rank-1 updates
     // with the row broadcast from LDS.
-#ifndef AW_HESS_VALU
     // Dense part J_d' D J_d on the matrix cores (hess_dense_mfma above): every lower-triangle
     // entry (and the row padding) of s.L is written by exactly one plain store, then the sparse
     // rows are added with LDS atomics as below.
@@ -852,22 +689,11 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
     wsync();
     hess_dense_mfma<NV>(m, s, lane);
     wsync();
-#else
-    {
-      constexpr int n4 = (tri(NV) + 3) / 4;
-      float4* Lz = reinterpret_cast<float4*>(s.L);
-      for (int i = lane; i < n4; i += 64) Lz[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    wsync();
-#endif
 #pragma unroll
     for (int h = 0; h < NRL; h++) {
       int r = lane + 64 * h;
       if (r < nefc) {
         float w = rr[h].st == S_QUAD ? rr[h].D : 0.f;
-#ifdef AW_HESS_VALU
-        s.rowbuf[r] = w;
-#endif
         if (r < s.nsparse && w != 0.f) {
           int i0 = s.efc_i0[r], i1 = s.efc_i1[r];
           float v0 = s.efc_v0[r], v1 = s.efc_v1[r];
@@ -893,45 +719,9 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
           if (4 * q + t < NV) H[4 * q + t] = Mrow[4 * q + t] + vv[t];
       }
     }
-#endif
     AW_PROF(s, PR_NT_HOFFD);
-#ifdef AW_HESS_VALU
-    const int nd = s.ndense, ndl = nd < JL ? nd : JL;
-    for (int d = 0; d < ndl; d++) {
-      float w = s.rowbuf[s.nsparse + d];
-      if (w == 0.f) continue;
-      float av = w * s.J[d][li];
-#pragma unroll
-      for (int k = 0; k < NV; k++) H[k] = fmaf(av, s.J[d][k], H[k]);
-    }
-    if (nd > JL) {
-      // spill rows: the row's entry per lane (coalesced), broadcast with readlane
-      gp_t<const float> Jg = jspill_row(m, s, JL);
-      for (int d = JL; d < nd; d++, Jg += VS) {
-        float w = s.rowbuf[s.nsparse + d];
-        if (w == 0.f) continue;
-        const float jl = Jg[li];
-        const float av = w * jl;
-#pragma unroll
-        for (int k = 0; k < NV; k++) H[k] = fmaf(av, rlane(jl, k), H[k]);
-      }
-    }
-#endif
     wsync();
     AW_PROF(s, PR_NT_HESS);
-#ifdef AW_SPLIT_FACTOR
-    // opt-in: on the A/B the uniform coupling test + the second unrolled factor cost more than the
-    // shorter chain saves (-1.0 % random, -0.4 % DAPG, r03zb; decoupled in most substeps or not,
-    // the code-size growth of +1.4 k instructions lands on the instruction cache)
-    if constexpr (SPLIT > 0 && NV - SPLIT + AW_CHOL_LA <= SPLIT) {
-      // hand / object blocks decoupled (no hand-object contact row in H): the block-split factor
-      bool cpl = false;
-#pragma unroll
-      for (int k = 0; k < SPLIT; k++) cpl = cpl || H[k] != 0.f;
-      if (__ballot(lane >= SPLIT && lane < NV && cpl)) chol_factor<NV>(H, lane, invd, s);
-      else chol_factor_split<NV, SPLIT>(H, lane, invd, s);
-    } else
-#endif
     chol_factor<NV>(H, lane, invd, s);
     chol_store<NV>(H, lane, s);
     wsync();
@@ -1015,7 +805,6 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
 
 // ---------------------------------------------------------------------------------------
 // noslip: PGS over frictionloss rows and opposing pyramid-edge pairs, no regularisation
-#ifndef AW_NOSLIP_PAIRS
 // Row space (default).  mj_solNoSlip is projected Gauss-Seidel over the noslip rows: the
 // frictionloss row of every dof (J = e_d) and the opposing pyramid-edge pairs.  A pair's update
 // keeps f1 + f2 and moves f1 - f2 (d2 = -d1), so it acts through its difference row
@@ -1095,48 +884,6 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
     }
     col = a;
   };
-#ifdef AW_NS_SETUP_OLD
-  // pairs with K = jd . xd >= MINVAL, in row order: the first NPL get a lane (constants there, xd
-  // to the transpose buffer), the rest keep their constants in lane p - NPL
-  int npr = 0;
-  int ex_e = 0;
-  float ex_ca = 0.f, ex_cb = 0.f, ex_K = 0.f, ex_fa = 0.f, ex_fb = 0.f;
-  for (int e = 0; e + 1 < ndense; e++) {
-    if (!(s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1)) continue;
-    float jd, xd;
-    pair_col(e, jd, xd);
-    const float K = wave_sum(jd * xd);
-    if (!(K >= MINVAL)) continue;
-    const int p = npr++;
-    const float ik = 1.0f / K;
-    const float ard = s.efc_aref[nsparse + e] - s.efc_aref[nsparse + e + 1];
-    const float f1 = s.efc_force[nsparse + e], f2 = s.efc_force[nsparse + e + 1];
-    if (p < NPL) {
-      const float Sp = wave_sum(jd * R);   // jd . qacc
-      if (lane < NV) Xb[p * XS + lane] = xd;
-      if (lane == NV + p) { rowe = e; ca = ik; cb = ard * ik; diag = K; fa = f1; fb = f2; R = Sp; }
-    } else if (lane == p - NPL) {
-      ex_e = e; ex_ca = ik; ex_cb = ard * ik; ex_K = K; ex_fa = f1; ex_fb = f2;
-    }
-  }
-  const int npl = npr < NPL ? npr : NPL;
-  float jq[NV];
-  (void)jq;
-  wsync();
-  // pair lanes: the dof columns of their row, xd_q, from the transpose buffer
-  if (lane >= NV && lane < NV + npl) {
-    const float* xr = Xb + (lane - NV) * XS;
-#pragma unroll
-    for (int q = 0; q < XS / 4; q++) {
-      const float4 v = *reinterpret_cast<const float4*>(xr + 4 * q);
-      const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int t = 0; t < 4; t++)
-        if (4 * q + t < NV) Am[4 * q + t] = vv[t];
-    }
-  }
-  wsync();
-#else
   // candidate pairs: first rows e of opposing pyramid-edge pairs, in row order, found by a ballot
   // over the dense rows (no serial scan).  The first NPL get a lane: xd = inv(M) jd' goes to the
   // transpose buffer here, and the pair lane forms its own constants below (K = jd . xd and
@@ -1154,16 +901,13 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
   int npr = 0;
   int ex_e = 0;
   float ex_ca = 0.f, ex_cb = 0.f, ex_K = 0.f, ex_fa = 0.f, ex_fb = 0.f;
-#ifndef AW_NS_X_VALU
   // with >= 4 pair lanes the lane pairs' xd = inv(M) jd' come from one MFMA product below
-  // (DAPG +2.7 %, random +-0, r03zg; -DAW_NS_X_VALU keeps the per-pair VALU products)
+  // (DAPG +2.7 %, random +-0, r03zg, against per-pair VALU products)
   const int npr_all = __popcll(cmask[0]) + __popcll(cmask[1]);
   // (hammer; relocate's 36 x 36 inv(M) does not fit the staging area, door / pen have 34 pair lanes)
-  constexpr bool X_FIT = NPL <= 32 && NV * XS * sizeof(float) <= offsetof(Env, qpos);
+  // the staging writes NV rows of inv(M) and the product writes rows p < 32 of the buffer
+  constexpr bool X_FIT = NPL <= 32 && (NV > 32 ? NV : 32) * XS * sizeof(float) <= offsetof(Env, qpos);
   const bool x_mfma = X_FIT && (npr_all < NPL ? npr_all : NPL) >= 4;
-#else
-  constexpr bool x_mfma = false;
-#endif
 #pragma unroll
   for (int h = 0; h < 2; h++) {
     unsigned long long mk = cmask[h];
@@ -1193,8 +937,8 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
       }
     }
   }
-#ifndef AW_NS_X_VALU
   if constexpr (X_FIT) {
+    static_assert(32 * XS * sizeof(float) <= offsetof(Env, qpos), "x_mfma output rows exceed the staging area");
     if (x_mfma) {
       // X = inv(M) Jd' (NV x npl, K = NV) on the matrix cores: A rows are inv(M)'s rows (each dof
       // lane stages its row Am in the transpose buffer), B columns the pairs' difference rows
@@ -1266,7 +1010,6 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
         }
     }
   }
-#endif
   const int npl = npr < NPL ? npr : NPL;
   if (lane < NV) s.rowbuf[lane] = R;   // qacc for the pair lanes' jd . qacc (rowbuf is rewritten after noslip)
   wsync();
@@ -1318,34 +1061,11 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
     }
   }
   wsync();
-#endif
   // pair columns of every lane's row: dof lanes read xd_p[lane] back from the transpose buffer;
   // pair lanes form G_q[p] = jd_q . xd_p from their difference row (registers) and xd_p
   // (broadcast reads of the buffer)
   float Ap[NPL];
-#ifdef AW_NS_G_RECOMPUTE
-#pragma unroll
-  for (int p = 0; p < NPL; p++) {
-    if (p < npl) {
-      float jd, col;
-      pair_col(rlane_i(rowe, NV + p), jd, col);
-      Ap[p] = col;
-    }
-  }
-#else
   {
-#ifdef AW_NS_SETUP_OLD
-    const int e = lane >= NV && lane < NV + npl ? rowe : 0;
-    if (e + 1 < JL) {
-#pragma unroll
-      for (int d = 0; d < NV; d++) jq[d] = s.J[e][d] - s.J[e + 1][d];
-    } else {
-      auto jat = [&](int r, int d) { return r < JL ? s.J[r][d] : jspill_row(m, s, r)[d]; };
-#pragma unroll
-      for (int d = 0; d < NV; d++) jq[d] = jat(e, d) - jat(e + 1, d);
-    }
-#endif
-#ifndef AW_NS_G_VALU
     // G = Jd Xd' (npl x npl, K = NV) on the matrix cores when there are enough pairs: A rows are
     // the pairs' difference rows jd_q = J_e - J_e+1 read from the Jacobian (LDS rows / global
     // spill rows; the pair's row index e comes from its lane by a shuffle), B rows the xd_p in
@@ -1422,9 +1142,6 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
         wsync();
       }
     }
-#else
-    constexpr bool g_mfma = false;
-#endif
 #pragma unroll
     for (int p = 0; p < NPL; p++) {
       if (p < npl && !g_mfma) {
@@ -1442,7 +1159,6 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
       }
     }
   }
-#endif
   AW_PROF(s, PR_NS_SETUP);
   if (lane == 0) s.it_noslip = 0;
   const float scale = 1.f / (m.meaninertia * (float)(NV > 1 ? NV : 1));
@@ -1455,11 +1171,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
     auto step = [&](float a_c, int c) {
       const float y = fmaf(-R, ca, cb);
       const float d = rlane(__builtin_amdgcn_fmed3f(y, lo, hi), c);
-#ifdef AW_NS_SELMASK
-      ysv = sel_lane(ysv, y, c);
-#else
       ysv = lane == c ? y : ysv;
-#endif
       R = fmaf(a_c, d, R);
     };
 #pragma unroll
@@ -1500,227 +1212,6 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
   }
   wsync();
 }
-#else
-// Pair space (A/B variant, -DAW_NOSLIP_PAIRS).
-template <int TASK, bool KEEP_D>
-AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mrow)[Tree<TASK>::NV], float& qacc) {
-  const int lane = lane_ns;
-  constexpr int NV = Tree<TASK>::NV;
-  const int nsparse = s.nsparse, ndense = s.ndense;
-  // inv(M) from the tree factor of M (aw_tree.h): lane i keeps row i of inv(M) in VGPRs
-  // (symmetric: row == column)
-  float Mi[NV];
-  {
-    float row[NV];
-#pragma unroll
-    for (int k = 0; k < NV; k++) row[k] = Mrow[k];
-    float invd;
-    tree_factor<TASK>(row, invd, lane);
-    tree_inverse<TASK>(row, invd, lane, Mi);
-  }
-  if (lane >= NV) {
-#pragma unroll
-    for (int k = 0; k < NV; k++) Mi[k] = 0.f;
-  }
-  const int li = lane < NV ? lane : 0;
-  const float lm = lane < NV ? 1.f : 0.f;
-  wsync();
-  AW_PROF(s, PR_NS_MINV);
-  // forces: frictionloss rows per dof lane, pyramid-edge pairs per pair lane
-  const bool use_fl = !(m.disableflags & DSBL_FRICTIONLOSS);
-  float ffl = 0.f;
-  // per-dof-lane constants of the frictionloss row of that dof (lane d owns row fl_row[d])
-  float fl_aref = 0.f, fl_lim = 0.f, fl_A = 1.f, fl_invA = 0.f;
-  float fl_c = 0.f;   // ffl + aref / A: the proposal is med3(fl_c - qacc / A, -lim, lim)
-  {
-    float dg = 0.f;   // inv(M)[lane][lane]
-#pragma unroll
-    for (int k = 0; k < NV; k++) dg = k == lane ? Mi[k] : dg;
-    const int row = lane < NV ? MD(fl_row, lane) : -1;
-    const bool has = row >= 0 && row < nsparse;
-    if (has) ffl = s.efc_force[row];
-    if (use_fl && has && dg >= MINVAL) {
-      fl_aref = s.efc_aref[row];
-      fl_lim = s.efc_floss[row];
-      fl_A = dg;
-      fl_invA = 1.0f / dg;
-    } else {
-      // lanes without an active row propose their own force back (dl = 0 exactly): invA 0, no clamp
-      fl_invA = 0.f;
-      fl_lim = 3.0e38f;
-    }
-    fl_c = fmaf(fl_aref, fl_invA, ffl);
-  }
-  qacc = lane < NV ? qacc : 0.f;
-  const float scale = 1.f / (m.meaninertia * (float)(NV > 1 ? NV : 1));
-  // opposing pyramid-edge pairs (e, e+1) in row order.  A pair's update keeps f1 + f2 (the
-  // normal force) and moves x = f1 - f2, so d2 = -d1 and everything it needs is the difference
-  // of its two rows: jd = J_e - J_e+1 and xd = inv(M) jd' (dof vectors), K = jd . xd,
-  // r1 - r2 = jd . qacc - (aref_e - aref_e+1).  Pairs with K >= MINVAL are compacted; pair p's
-  // constants and its two forces live in lane p.  jd / xd of the first NSP_CACHE pairs stay in
-  // VGPRs, the next NSP_LDS are parked in dead LDS, the rest are rebuilt each sweep.
-  int npr = 0, pr_e = 0;
-  float pr_ik = 0.f, pr_aik = 0.f, pr_ard = 0.f, pr_hk = 0.f, pf1 = 0.f, pf2 = 0.f;
-  float c_jd[NSP_CACHE], c_xd[NSP_CACHE];
-#pragma unroll
-  for (int p = 0; p < NSP_CACHE; p++) c_jd[p] = c_xd[p] = 0.f;
-  // J row d at this lane's dof
-  auto jval = [&](int d) { return lm * (d < JL ? s.J[d][li] : jspill_row(m, s, d)[li]); };
-  // jd at this lane's dof and (inv(M) jd')_lane for the pair (e, e+1)
-  auto pair_rows = [&](int e, float& jd, float& xd) {
-    float a = 0.f;
-    if (e + 1 < JL) {
-#pragma unroll
-      for (int j = 0; j < NV; j++) a = fmaf(Mi[j], s.J[e][j] - s.J[e + 1][j], a);
-      jd = lm * (s.J[e][li] - s.J[e + 1][li]);
-    } else {
-      const float dl = jval(e) - jval(e + 1);
-#pragma unroll
-      for (int j = 0; j < NV; j++) a = fmaf(Mi[j], rlane(dl, j), a);
-      jd = dl;
-    }
-    xd = a;
-  };
-  for (int e = 0; e + 1 < ndense; e++) {
-    if (!(s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1)) continue;
-    float jd, xd;
-    pair_rows(e, jd, xd);
-    const float K = wave_sum(jd * xd);
-    if (!(K >= MINVAL)) continue;
-    const int p = npr++;
-    if (lane == p) {
-      pr_e = e; pr_ik = 1.0f / K; pr_hk = 0.5f * K;
-      pr_ard = s.efc_aref[nsparse + e] - s.efc_aref[nsparse + e + 1];
-      pr_aik = pr_ard * pr_ik;
-      pf1 = s.efc_force[nsparse + e];
-      pf2 = s.efc_force[nsparse + e + 1];
-    }
-#pragma unroll
-    for (int q = 0; q < NSP_CACHE; q++)
-      if (q == p) { c_jd[q] = jd; c_xd[q] = xd; }
-    if (p >= NSP_CACHE && p < NSP_CACHE + NSP_LDS<KEEP_D> && lane < MAXV) {
-      float* slot = xpark_slot<KEEP_D>(s, p - NSP_CACHE);
-      slot[lane] = jd;
-      slot[MAXV + lane] = xd;
-    }
-  }
-  // Pair space of the cached pairs: S (lane q) = jd_q . qacc is the residual that pair q's update
-  // reads, and an update d1 of pair p moves it by G_p d1 with G_p (lane q) = jd_q . xd_p -- a
-  // constant of the solve.  So a pair's step is fma -> med3 -> readlane -> fma on the serial chain
-  // (no wave reduction), and S is recomputed from qacc once per sweep, after the dry-friction rows.
-  const int ncache = npr < NSP_CACHE ? npr : NSP_CACHE;
-  float G[NSP_CACHE];
-  {
-    // lane q < ncache: jd_q at every dof (its two rows, from LDS or the spill block)
-    const bool own = lane < ncache;
-    const int e = own ? pr_e : 0;
-    float jq[NV];
-    if (e + 1 < JL) {
-#pragma unroll
-      for (int d = 0; d < NV; d++) jq[d] = s.J[e][d] - s.J[e + 1][d];
-    } else {
-      auto jat = [&](int r, int d) { return r < JL ? s.J[r][d] : jspill_row(m, s, r)[d]; };
-#pragma unroll
-      for (int d = 0; d < NV; d++) jq[d] = jat(e, d) - jat(e + 1, d);
-    }
-#pragma unroll
-    for (int p = 0; p < NSP_CACHE; p++) {
-      float g = 0.f;
-      if (p < ncache) {
-#pragma unroll
-        for (int d = 0; d < NV; d++) g = fmaf(jq[d], rlane(c_xd[p], d), g);
-      }
-      G[p] = own ? g : 0.f;
-    }
-  }
-  wsync();
-  AW_PROF(s, PR_NS_SETUP);
-  if (lane == 0) s.it_noslip = 0;
-  for (int it = 0; it < m.noslip_iterations; it++) {
-    const int lane = opaque(lane_ns);   // per-sweep lane id: the dof / pair compares stay in the sweep
-    AW_PROF_ADD(s, PR_NOSLIP_IT, 1);
-    if (lane == 0) s.it_noslip = it + 1;
-    // dry-friction rows in dof order (Gauss-Seidel).  Every lane evaluates the projected update
-    // of its own row against the current qacc; step d keeps lane d's (x and the qacc it saw, for
-    // the force and the improvement after the loop).  Lanes without an active row propose
-    // exactly zero (branch-free).  Serial chain per row: fma -> med3 -> sub -> readlane -> fma.
-    float xsv = ffl, qsv = 0.f;
-#pragma unroll
-    for (int d = 0; d < NV; d++) {
-      const float x = __builtin_amdgcn_fmed3f(fmaf(-qacc, fl_invA, fl_c), -fl_lim, fl_lim);
-      const float delta = rlane(x - ffl, d);
-      if (lane == d) { xsv = x; qsv = qacc; }
-      qacc = fmaf(Mi[d], delta, qacc);
-    }
-    float imp_l;
-    {
-      const float dl = xsv - ffl;
-      imp_l = (qsv - fl_aref) * dl + 0.5f * fl_A * dl * dl;
-      ffl = xsv;
-      fl_c = fmaf(fl_aref, fl_invA, ffl);
-    }
-    // opposing pyramid-edge pairs, in row order (branch-free: a zero update is an exact no-op).
-    // x' = clamp(x - 2 rd / K, -sum, sum) with x = f1 - f2, sum = f1 + f2 gives
-    // d1 = (x' - x) / 2 = med3(-rd / K, -f1, f2); the improvement is rd d1 + K d1^2 / 2.
-    if (ncache > 0) {
-      float S = 0.f;
-#pragma unroll
-      for (int c = 0; c < NSP_CACHE; c += 4) {
-        if (c < ncache) {
-#pragma unroll
-          for (int p = c; p < c + 4 && p < NSP_CACHE; p++) {
-            const float sp = wave_sum(c_jd[p] * qacc);
-            S = lane == p ? sp : S;
-          }
-        }
-      }
-      float d1sv = 0.f, ssv = 0.f;
-#pragma unroll
-      for (int p = 0; p < NSP_CACHE; p++) {
-        if (p < ncache) {
-          const float d1v = __builtin_amdgcn_fmed3f(fmaf(-S, pr_ik, pr_aik), -pf1, pf2);   // lane p's
-          const float d1 = rlane(d1v, p);
-          if (lane == p) { d1sv = d1v; ssv = S; }
-          S = fmaf(G[p], d1, S);
-          qacc = fmaf(c_xd[p], d1, qacc);
-        }
-      }
-      imp_l += (ssv - pr_ard) * d1sv + pr_hk * d1sv * d1sv;
-      pf1 += d1sv;
-      pf2 -= d1sv;
-    }
-    // pairs past the VGPR cache: the residual by a wave reduction
-    for (int p = NSP_CACHE; p < npr; p++) {
-      float jd, xd;
-      if (p < NSP_CACHE + NSP_LDS<KEEP_D>) {   // parked in LDS
-        const float* slot = xpark_slot<KEEP_D>(s, p - NSP_CACHE);
-        jd = lane < MAXV ? slot[lane] : 0.f;
-        xd = lane < MAXV ? slot[MAXV + lane] : 0.f;
-      } else {
-        pair_rows(rlane_i(pr_e, p), jd, xd);
-      }
-      const float sq = wave_sum(jd * qacc);
-      const float d1 = __builtin_amdgcn_fmed3f(fmaf(-sq, rlane(pr_ik, p), rlane(pr_aik, p)),
-                                               -rlane(pf1, p), rlane(pf2, p));
-      qacc = fmaf(xd, d1, qacc);
-      if (lane == p) {
-        imp_l += (sq - pr_ard) * d1 + pr_hk * d1 * d1;
-        pf1 += d1;
-        pf2 -= d1;
-      }
-    }
-    if (-wave_sum(imp_l) * scale < m.noslip_tolerance) break;
-  }
-  AW_PROF(s, PR_NS_ITER);
-  if (lane < NV && MD(fl_row, lane) >= 0 && MD(fl_row, lane) < nsparse) s.efc_force[MD(fl_row, lane)] = ffl;
-  if (lane < npr) {
-    s.efc_force[nsparse + pr_e] = pf1;
-    s.efc_force[nsparse + pr_e + 1] = pf2;
-  }
-  wsync();
-}
-
-#endif
 
 // ---------------------------------------------------------------------------------------
 // mju_rayGeom for site shapes: distance to the first crossing at t >= 0, or -1
