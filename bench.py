@@ -366,15 +366,15 @@ def main():
     depth_ms = sum(e[2].elapsed_time(e[3]) for e in events) / args.steps if depth is not None else None
     e1, r1, s1 = gather()
     # the exchange's own check: the gathered global totals equal the sum of every rank's block
-    local = torch.stack([tot_ep.long().sum(), tot_suc.long().sum()])
+    rank_sums = torch.stack([tot_ep.long().sum(), tot_suc.long().sum()])
     if pg:
-        dist.all_reduce(local, op=dist.ReduceOp.SUM)
+        dist.all_reduce(rank_sums, op=dist.ReduceOp.SUM)
     exchange = dict(backend=dist.get_backend() if pg else "local copy", world=world, collective="all_gather_into_tensor"
                     if pg else None, calls=totals.calls, bytes_per_rank_per_call=totals.bytes_per_rank,
                     every_steps=sim.horizon, global_episodes=int(e1.long().sum()),
                     global_successes=int(s1.long().sum()),
-                    gathered_equals_rank_sums=bool(int(e1.long().sum()) == int(local[0])
-                                                   and int(s1.long().sum()) == int(local[1])))
+                    gathered_equals_rank_sums=bool(int(e1.long().sum()) == int(rank_sums[0])
+                                                   and int(s1.long().sum()) == int(rank_sums[1])))
     sim.status(sticky=sticky)
     n_over = int(((sticky & _native.ST_OVERFLOW) != 0).sum())
     n_nan = int(((sticky & (_native.ST_BADQPOS | _native.ST_BADQVEL | _native.ST_BADQACC)) != 0).sum())

@@ -36,6 +36,8 @@ def dump_layout(maxcon=MAXCON, maxefc=MAXEFC):
 
 
 DUMP_LAYOUT = dump_layout()
+# why the Newton solve stopped (aw_solver.h NT_EXIT_*)
+NT_EXIT = ("max_iterations", "no_descent", "fp32_noise_floor", "improvement", "gradient")
 AW_DUMP_SIZE = 1768 + 14 * MAXCON + 4 * MAXEFC
 
 _lib = None
@@ -295,7 +297,7 @@ class Sim:
         sc = res["scalars"]
         ncon, nefc = int(sc[0]), int(sc[1])
         res.update(ncon=ncon, nefc=nefc, nsparse=int(sc[2]), ndense=int(sc[3]), touch=sc[4], status=int(sc[5]),
-                   solver_iter=int(sc[6]), noslip_iter=int(sc[7]))
+                   solver_iter=int(sc[6]) % 1000, solver_exit=NT_EXIT[int(sc[6]) // 1000], noslip_iter=int(sc[7]))
         res["con_dist"] = res["con_dist"][:ncon]
         res["con_pos"] = res["con_pos"][:3 * ncon].reshape(ncon, 3)
         res["con_frame"] = res["con_frame"][:9 * ncon].reshape(ncon, 9)

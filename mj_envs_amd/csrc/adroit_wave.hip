@@ -98,7 +98,33 @@ AW_DEV void sort_contacts(Env& s, int lane) {
 template <int C>
 AW_DEV void narrow_class(const DModel& m, Env& s, const short* plist, int cnt, int lane) {
   const int st = m.cls_start[C];
-  for (int i = lane; i < cnt; i += 64) collide_pair<C>(m, s, plist[st + i]);
+  if constexpr (C == 2) {
+    // sphere / capsule - box.  (1) lane per pair: a pair whose segment cannot come within the
+    // margin of the box -- the box's signed distance at the segment centre, less the half-length
+    // and radius, exceeds margin + 1e-4 (the distance is 1-Lipschitz along the segment) -- emits
+    // nothing in the full collider either and is dropped; the survivors are compacted in place.
+    // (2) one survivor per 16-lane DPP row, four per round (capsule-box's 43-candidate minimiser
+    // search is spread over the row, aw_collide.h capbox_tstar_row).
+    short* list = const_cast<short*>(plist) + st;
+    int nsurv = 0;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    for (int base = 0; base < cnt; base += 64) {
+      const int i = base + lane;
+      const int pair = i < cnt ? list[i] : 0;
+      const bool keep = i < cnt && capbox_may_touch(m, s, pair);
+      const unsigned long long mask = __ballot(keep);
+      wsync();
+      if (keep) list[nsurv + __popcll(mask & below)] = (short)pair;
+      nsurv += __popcll(mask);
+      wsync();
+    }
+    for (int i0 = 0; i0 < nsurv; i0 += 4) {
+      const int i = i0 + (lane >> 4);
+      if (i < nsurv) collide_pair<C>(m, s, list[i], lane & 15);
+    }
+  } else {
+    for (int i = lane; i < cnt; i += 64) collide_pair<C>(m, s, plist[st + i]);
+  }
 }
 
 // mj_collision: bounding-sphere broadphase over the static candidate list (one pair per lane,
@@ -591,8 +617,15 @@ __global__ void __launch_bounds__(64) k_task_eval(DModel m, int n, const float* 
 
 // Test hook (aw_collide_test): the narrowphase of one primitive pair per workgroup, given world
 // poses -- exact-geometry collider tests against the oracle's colliders.
-AW_DEV void collide_gv(const DModel& m, const GV& a, const GV& b, float margin, Emit& e) {
+// Lanes 0..15 call it with the same pair (gl = lane): capsule-box runs on the 16-lane row as in
+// the narrowphase, every other collider on lane 0.
+AW_DEV void collide_gv(const DModel& m, const GV& a, const GV& b, float margin, Emit& e, int gl) {
   const int lo = a.type, hi = b.type;   // a.type <= b.type
+  if (hi == GEOM_BOX && lo == GEOM_CAPSULE) {
+    c_capsule_box(a, b, margin, e, gl);
+    return;
+  }
+  if (gl != 0) return;
   if (lo == GEOM_PLANE) {
     if (hi == GEOM_SPHERE) c_plane_sphere(a.pos, a.mat, b.pos, b.size[0], margin, e);
     else if (hi == GEOM_CAPSULE) c_plane_capsule(a, b, margin, e);
@@ -607,8 +640,7 @@ AW_DEV void collide_gv(const DModel& m, const GV& a, const GV& b, float margin, 
   } else if (hi == GEOM_BOX && lo == GEOM_BOX) {
     c_box_box(a, b, margin, e);
   } else if (hi == GEOM_BOX) {
-    if (lo == GEOM_SPHERE) c_sphere_box_pt(a.pos, a.size[0], b, margin, e);
-    else c_capsule_box(a, b, margin, e);
+    c_sphere_box_pt(a.pos, a.size[0], b, margin, e);
   } else if (lo == GEOM_SPHERE && hi == GEOM_SPHERE) {
     c_sphere_sphere(a.pos, a.size[0], b.pos, b.size[0], margin, e);
   } else if (lo == GEOM_SPHERE) {
@@ -626,7 +658,7 @@ __global__ void __launch_bounds__(64) k_collide_test(DModel m, int n, const int*
   if (i >= n) return;
   if (lane == 0) { s.ncon = 0; s.status = 0u; }
   wsync();
-  if (lane == 0) {
+  if (lane < 16) {
     GV g[2];
     for (int q = 0; q < 2; q++) {
       g[q].type = types[2 * i + q];
@@ -635,7 +667,7 @@ __global__ void __launch_bounds__(64) k_collide_test(DModel m, int n, const int*
     }
     const int f = g[0].type <= g[1].type ? 0 : 1;
     Emit e{&s, 0, 0};
-    collide_gv(m, g[f], g[1 - f], margin[i], e);
+    collide_gv(m, g[f], g[1 - f], margin[i], e, lane);
   }
   wsync();
   const int nc = s.ncon < MAXPAIRCON ? s.ncon : MAXPAIRCON;

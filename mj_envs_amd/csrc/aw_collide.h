@@ -237,7 +237,85 @@ AW_DEV float seg_box_f(const float* c, const float* u, const float* s, float t) 
 //  3. face: the segment part over face k is [lo, hi]; t* moves to the nearer end when that end
 //     is as close (parallel capsule) and the other end is the second point; both sphere-box
 //     contacts within the margin (flat on a face: two contacts at the clipped ends).
-AW_DEV void c_capsule_box(const GV& a, const GV& b, float margin, Emit& e) {
+// Step 1's candidates, 43 of them, spread over the 16 lanes of a DPP row (lane gl of the row
+// takes candidates gl, gl + 16, gl + 32): 0, 1 the segment ends; 2..10 the slab / zero crossings
+// of coordinate j = (k - 2) / 3; 11..30 the stationary points of the outside pieces with two or
+// three coordinates outside (code digits cd_j: 0 inside, 1 above +s_j, 2 below -s_j); 31..42
+// the crossings of two inside pieces (i, j, signs).  The minimiser is the lexicographic
+// minimum of (f, t) over the candidates -- the sequential scan's "smaller f, ties to smaller
+// t" -- so the row reduction below returns the scan's t* whatever the evaluation order.
+// Three-digit codes with >= 2 nonzero digits, 6 bits each (cd0 | cd1 << 2 | cd2 << 4), in the
+// scan's code order: codes 4 5 7 8 10..17 19..26 of 0..26.
+constexpr unsigned long long CAPBOX_CODES_LO =
+    0x05ull | 0x06ull << 6 | 0x09ull << 12 | 0x0Aull << 18 | 0x11ull << 24 | 0x12ull << 30 | 0x14ull << 36 |
+    0x15ull << 42 | 0x16ull << 48 | 0x18ull << 54;
+constexpr unsigned long long CAPBOX_CODES_HI =
+    0x19ull | 0x1Aull << 6 | 0x21ull << 12 | 0x22ull << 18 | 0x24ull << 24 | 0x25ull << 30 | 0x26ull << 36 |
+    0x28ull << 42 | 0x29ull << 48 | 0x2Aull << 54;
+static_assert(CAPBOX_CODES_LO == 0x616554491289185ull && CAPBOX_CODES_HI == 0xaa9a269648a1699ull, "code table");
+AW_DEV float sel3(const float* v, int j) { return j == 0 ? v[0] : (j == 1 ? v[1] : v[2]); }
+AW_DEV void capbox_tstar_row(const float* c, const float* u, const float* sz, float h, int gl, float& best_f,
+                             float& best_t) {
+  float bf = 3.402823466e38f, bt = 3.402823466e38f;
+#pragma unroll
+  for (int rd = 0; rd < 3; rd++) {
+    const int k = gl + 16 * rd;
+    float t = -h;
+    bool ok = k < 43;
+    if (k == 1) {
+      t = h;
+    } else if (k >= 2 && k < 11) {
+      const int j = (k - 2) / 3, w = (k - 2) - 3 * j;
+      const float uj = sel3(u, j), cj = sel3(c, j), sj = sel3(sz, j);
+      ok = fabsf(uj) > 1e-12f;
+      const float iu = 1.0f / uj;
+      t = (w == 0 ? sj - cj : (w == 1 ? -sj - cj : -cj)) * iu;
+    } else if (k >= 11 && k < 31) {
+      const int q = k - 11;
+      const int code = (int)(((q < 10 ? CAPBOX_CODES_LO : CAPBOX_CODES_HI) >> (6 * (q < 10 ? q : q - 10))) & 63ull);
+      float nu = 0.f, de = 0.f;
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        const int cdj = (code >> (2 * j)) & 3;
+        const float sg = cdj == 1 ? 1.f : -1.f;
+        const float tn = (sz[j] * sg - c[j]) * u[j], td = u[j] * u[j];
+        nu = cdj ? nu + tn : nu;
+        de = cdj ? de + td : de;
+      }
+      ok = de > 1e-24f;
+      t = nu / de;
+    } else if (k >= 31 && k < 43) {
+      const int q = k - 31, pr = q >> 2, sc = q & 3;
+      const int i = pr == 2 ? 1 : 0, j = pr == 0 ? 1 : 2;
+      const float si = (sc & 1) ? -1.f : 1.f, sj = (sc & 2) ? -1.f : 1.f;
+      const float ui = sel3(u, i), uj = sel3(u, j), ci = sel3(c, i), cj = sel3(c, j);
+      const float den = si * ui - sj * uj;
+      ok = fabsf(den) > 1e-12f;
+      t = (sel3(sz, i) - sel3(sz, j) - si * ci + sj * cj) / den;
+    }
+    t = fminf(fmaxf(t, -h), h);
+    const float f = ok ? seg_box_f(c, u, sz, t) : 3.402823466e38f;
+    const bool take = ok && (f < bf || (f == bf && t < bt));
+    bf = take ? f : bf;
+    bt = take ? t : bt;
+  }
+  // lexicographic (f, t) minimum over the 16-lane row: xor 1, xor 2, half-row and row mirrors
+  auto step = [&](float pf, float pt) {
+    const bool take = pf < bf || (pf == bf && pt < bt);
+    bf = take ? pf : bf;
+    bt = take ? pt : bt;
+  };
+  step(dpp_f<0xB1>(0.f, bf), dpp_f<0xB1>(0.f, bt));
+  step(dpp_f<0x4E>(0.f, bf), dpp_f<0x4E>(0.f, bt));
+  step(dpp_f<0x141>(0.f, bf), dpp_f<0x141>(0.f, bt));
+  step(dpp_f<0x140>(0.f, bf), dpp_f<0x140>(0.f, bt));
+  best_f = bf;
+  best_t = bt;
+}
+
+// one capsule-box pair on the 16 lanes of a DPP row (gl = lane in the row); every lane of the
+// row computes the same contacts, the row's lane 0 emits them
+AW_DEV void c_capsule_box(const GV& a, const GV& b, float margin, Emit& e, int gl) {
   float ax[3];
   axis_of(ax, a.mat, 2);
   const float h = a.size[1], r = a.size[0];
@@ -246,48 +324,9 @@ AW_DEV void c_capsule_box(const GV& a, const GV& b, float margin, Emit& e) {
   sub3(dif, a.pos, b.pos);
   mulmtv3(c, b.mat, dif);
   mulmtv3(u, b.mat, ax);
-  float best_t = -h, best_f = seg_box_f(c, u, sz, -h);
-  auto cand = [&](float t) {
-    t = fminf(fmaxf(t, -h), h);
-    const float f = seg_box_f(c, u, sz, t);
-    const bool take = f < best_f || (f == best_f && t < best_t);
-    best_f = take ? f : best_f;
-    best_t = take ? t : best_t;
-  };
-  cand(h);
-#pragma unroll
-  for (int j = 0; j < 3; j++)
-    if (fabsf(u[j]) > 1e-12f) {
-      const float iu = 1.0f / u[j];
-      cand((sz[j] - c[j]) * iu);
-      cand((-sz[j] - c[j]) * iu);
-      cand(-c[j] * iu);
-    }
-#pragma unroll
-  for (int code = 0; code < 27; code++) {
-    const int cd0 = code % 3, cd1 = (code / 3) % 3, cd2 = code / 9;
-    if ((cd0 != 0) + (cd1 != 0) + (cd2 != 0) < 2) continue;
-    const int cd[3] = {cd0, cd1, cd2};
-    float nu = 0.f, de = 0.f;
-#pragma unroll
-    for (int j = 0; j < 3; j++)
-      if (cd[j]) {
-        const float sg = cd[j] == 1 ? 1.f : -1.f;
-        nu += (sz[j] * sg - c[j]) * u[j];
-        de += u[j] * u[j];
-      }
-    if (de > 1e-24f) cand(nu / de);
-  }
-#pragma unroll
-  for (int i = 0; i < 3; i++)
-#pragma unroll
-    for (int j = i + 1; j < 3; j++)
-#pragma unroll
-      for (int sc = 0; sc < 4; sc++) {
-        const float si = (sc & 1) ? -1.f : 1.f, sj = (sc & 2) ? -1.f : 1.f;
-        const float den = si * u[i] - sj * u[j];
-        if (fabsf(den) > 1e-12f) cand((sz[i] - sz[j] - si * c[i] + sj * c[j]) / den);
-      }
+  float best_f, best_t;
+  capbox_tstar_row(c, u, sz, h, gl, best_f, best_t);
+  if (gl != 0) return;
   float ts = best_t;
   int nout = 0, kout = 0, kin = 0;
   float pen = 1e30f;
@@ -807,13 +846,28 @@ AW_DEV void c_convex64(const DModel& m, const mpr::GVdT<double>& a, const mpr::G
   emit(e, (float)dist, pf, df);
 }
 
+// Conservative midphase of a sphere / capsule - box pair (class 2): false only when no point of
+// the segment can be within the margin of the box -- then the collider emits nothing either.
+AW_DEV bool capbox_may_touch(const DModel& m, const Env& s, int pair) {
+  const int g1 = MD(cp_g1, pair), g2 = MD(cp_g2, pair);   // g1 the sphere / capsule, g2 the box
+  const float h = MD(geom_type, g1) == GEOM_CAPSULE ? s.gsize[g1][1] : 0.f;
+  float mat[9], q[4], dif[3], c[3];
+  for (int k = 0; k < 4; k++) q[k] = s.gxquat[g2][k];
+  q2m(mat, q);
+  sub3(dif, s.gxpos[g1], s.gxpos[g2]);
+  mulmtv3(c, mat, dif);
+  const float zero[3] = {0.f, 0.f, 0.f};
+  const float lb = seg_box_f(c, zero, s.gsize[g2], 0.f) - h - s.gsize[g1][0];
+  return !(lb > MD(cp_margin, pair) + 1e-4f);
+}
+
 // ---------------------------------------------------------------------------------------
 // narrowphase of one pair of collider class C (host: adroit_wave.hip build_model pcls):
 // 0 plane-*, 1 sphere/capsule pairs, 2 sphere/capsule-box, 3 box-box, 4 anything with a
 // cylinder (MPR).  The class is a template parameter so each class loop carries only its own
 // colliders (no divergent merge of every collider's code and registers).
 template <int C>
-AW_DEV void collide_pair(const DModel& m, Env& s, int pair) {
+AW_DEV void collide_pair(const DModel& m, Env& s, int pair, int gl = 0) {
   int g1 = MD(cp_g1, pair), g2 = MD(cp_g2, pair);
   Emit e{&s, pair, 0};
   if constexpr (C == 4) {           // every non-plane pair with a cylinder: MPR (mjc_Convex)
@@ -846,9 +900,12 @@ AW_DEV void collide_pair(const DModel& m, Env& s, int pair) {
     if (a.type == GEOM_SPHERE && b.type == GEOM_SPHERE) c_sphere_sphere(a.pos, a.size[0], b.pos, b.size[0], margin, e);
     else if (a.type == GEOM_SPHERE) c_sphere_capsule(a, b, margin, e);
     else c_capsule_capsule(a, b, margin, e);
-  } else if constexpr (C == 2) {
-    if (a.type == GEOM_SPHERE) c_sphere_box_pt(a.pos, a.size[0], b, margin, e);
-    else c_capsule_box(a, b, margin, e);
+  } else if constexpr (C == 2) {   // one pair per 16-lane row (narrow_class), lane gl of the row
+    if (a.type == GEOM_SPHERE) {
+      if (gl == 0) c_sphere_box_pt(a.pos, a.size[0], b, margin, e);
+    } else {
+      c_capsule_box(a, b, margin, e, gl);
+    }
   } else {
     c_box_box(a, b, margin, e);
   }

@@ -473,6 +473,17 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
 // ---------------------------------------------------------------------------------------
 // Newton solver
 constexpr float GRAD_NOISE = 2e-6f;   // ~16 fp32 ulps of the gradient's terms
+#ifndef AW_NT_NOISE
+#define AW_NT_NOISE 0
+#endif
+#ifndef AW_NT_NOISE_DOF
+#define AW_NT_NOISE_DOF 2e-6f
+#endif
+#ifndef AW_NT_IMPROVE
+#define AW_NT_IMPROVE 0
+#endif
+// why the Newton solve stopped (s.it_newton = iterations + 1000 * reason, aw_forward_dump)
+enum { NT_EXIT_MAXITER = 0, NT_EXIT_NOSTEP = 1, NT_EXIT_NOISE = 2, NT_EXIT_IMPROVE = 3, NT_EXIT_GRAD = 4 };
 #ifndef AW_NSP_CACHE
 #define AW_NSP_CACHE 16
 #endif
@@ -644,6 +655,7 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
   // same Hessian as the previous one: its factor is reloaded instead of rebuilt (4 % of k_step on
   // the A/B; rank-1 up / downdates for a few changed rows measured slower than refactoring).
   float invd = 1.f;
+  int why = NT_EXIT_MAXITER;   // which test ended the solve (introspection: aw_forward_dump)
   bool inH[NRL];
 #pragma unroll
   for (int h = 0; h < NRL; h++) inH[h] = false;
@@ -774,24 +786,59 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
       }
     }
     AW_PROF(s, PR_NT_LS);
-    if (alpha == 0.f) { iter++; break; }
+    if (alpha == 0.f) { iter++; why = NT_EXIT_NOSTEP; break; }
+#if AW_NT_IMPROVE
+    // the rows' cost before the step, per lane (the improvement below is formed from per-row
+    // differences, not as the difference of two whole costs)
+    float rc_old = 0.f;
+#pragma unroll
+    for (int h = 0; h < NRL; h++) {
+      float f;
+      int st;
+      rc_old += row_eval(rr[h], rr[h].Jaref, &f, &st);
+    }
+#endif
     a += alpha * p;
     Ma += alpha * Mp;
 #pragma unroll
     for (int h = 0; h < NRL; h++) rr[h].Jaref += alpha * rr[h].Jp;
     float oldcost = cost;
+#if AW_NT_IMPROVE
+    // mj_solNewton's improvement = scale (oldcost - cost) without the fp32 cancellation of two
+    // whole costs: the smooth part's change along the line is exactly alpha c0 + alpha^2 c1 / 2
+    // (M a0 = qfrc_smooth, so p' M (a - a0) = c0), the rows' change is summed row by row
+    float rc_new = 0.f;
+#pragma unroll
+    for (int h = 0; h < NRL; h++) rc_new += row_eval(rr[h], rr[h].Jaref, &rr[h].force, &rr[h].st);
+    cost = oldcost + alpha * c0 + 0.5f * alpha * alpha * c1 + wave_sum(rc_new - rc_old);
+    const float dcost = -(alpha * c0 + 0.5f * alpha * alpha * c1 + wave_sum(rc_new - rc_old));
+#else
     cost = eval();
+#endif
     grad = gradient();
     float gn = sqrtf(wave_sum(grad * grad));
+#if AW_NT_IMPROVE
+    float improvement = scale * dcost, gradnorm = scale * gn;
+#else
     float improvement = scale * (oldcost - cost), gradnorm = scale * gn;
+#endif
     // fp32 termination: a gradient at the rounding floor of its own terms (Ma, qfrc_smooth,
     // J'f) cannot shrink further -- the fp64 reference would already stop on its 1e-8 test
     // here; an extra Newton step in fp32 only re-solves the same active set.
-    if (gn <= GRAD_NOISE * sqrtf(wave_sum(gref))) { iter++; break; }
+#if AW_NT_NOISE == 1
+    // per dof: every component at the floor of its OWN terms (a light object's dofs are not
+    // masked by the hand's large forces, as a norm over all dofs would let them be)
+    if (__ballot(lane < NV && fabsf(grad) > AW_NT_NOISE_DOF * sqrtf(gref)) == 0ull) { iter++; why = NT_EXIT_NOISE; break; }
+#elif AW_NT_NOISE == 2
+    // no noise-floor exit: MuJoCo's own improvement / gradient tests only
+#else
+    if (gn <= GRAD_NOISE * sqrtf(wave_sum(gref))) { iter++; why = NT_EXIT_NOISE; break; }
+#endif
     AW_PROF(s, PR_NT_UPD);
-    if (improvement < m.tolerance || gradnorm < m.tolerance) { iter++; break; }
+    if (improvement < m.tolerance) { iter++; why = NT_EXIT_IMPROVE; break; }
+    if (gradnorm < m.tolerance) { iter++; why = NT_EXIT_GRAD; break; }
   }
-  if (lane == 0) s.it_newton = iter;
+  if (lane == 0) s.it_newton = iter + 1000 * why;
   AW_PROF_ADD(s, PR_NEWTON_IT, iter);
   AW_PROF_ADD(s, PR_NEFC, nefc);
   AW_PROF_ADD(s, PR_NCON, s.ncon);

@@ -136,6 +136,79 @@ def _discrete_event(env_id, variation, o, params, qpos, qvel, warm, act, frame_s
     return False
 
 
+def _state_err(qg, vg, q_ref, v_ref):
+    """per-env max |dqpos|, max |dqvel| / (1 + |v|) and the one-step tolerance verdict"""
+    dq = np.abs(qg - q_ref)
+    dv = np.abs(vg - v_ref)
+    okq = (dq <= 2e-5 + 1e-5 * np.abs(q_ref)).all(axis=1)
+    okv = (dv <= 5e-3 * (1 + np.abs(v_ref))).all(axis=1)
+    return dq.max(axis=1), (dv / (1 + np.abs(v_ref))).max(axis=1), okq & okv
+
+
+def _err_report(label, eq, ev, ok):
+    """p50 / p99 / max of the per-case errors over the cases within tolerance (the misses are
+    classified separately): printed, and returned for the distribution gates below."""
+    eq, ev = np.asarray(eq)[ok], np.asarray(ev)[ok]
+    r = dict(qpos=np.percentile(eq, [50, 99, 100]) if eq.size else np.zeros(3),
+             qvel=np.percentile(ev, [50, 99, 100]) if ev.size else np.zeros(3))
+    print(f"{label}: |dqpos| p50 {r['qpos'][0]:.2e} p99 {r['qpos'][1]:.2e} max {r['qpos'][2]:.2e}; "
+          f"|dqvel|/(1+|v|) p50 {r['qvel'][0]:.2e} p99 {r['qvel'][1]:.2e} max {r['qvel'][2]:.2e}")
+    return r
+
+
+# Error-distribution gates (VERDICT r03 weak #7: the per-case tolerance sits orders of magnitude
+# above the achieved error, so a 10x regression could pass it).  Over the (env, step) cases within
+# tolerance, the p50 / p99 of max |dqpos| and max |dqvel| / (1 + |v|) must stay below these bounds,
+# set at ~4x the r04 measurements of the worst task / regime (profiles/r04*_pytest_gpu.txt).
+ERR_P50 = dict(qpos=1e-6, qvel=1e-4)
+ERR_P99 = dict(qpos=1.8e-5, qvel=4e-3)
+
+
+def _err_gate(r):
+    for k in ("qpos", "qvel"):
+        assert r[k][0] <= ERR_P50[k], (k, "p50", r[k][0])
+        assert r[k][1] <= ERR_P99[k], (k, "p99", r[k][1])
+
+
+def _fp32_sensitive(o, params, qpos, qvel, warm, act, trials=8, ulps=4, seed=0):
+    """Is the fp64 reference itself unstable at fp32 resolution here?  Re-runs the oracle's
+    env-step from the same state with every state component perturbed by up to `ulps` fp32 ulps
+    (relative 2^-23 each): True when some perturbed result leaves the one-step tolerance around
+    the unperturbed one -- the step sits on a discontinuity (a contact, row state or solver
+    decision switching) or is ill-conditioned within fp32 rounding of its input, so an fp32
+    simulation cannot be held to it."""
+    rng = np.random.default_rng(seed)
+    base = dict(qpos=qpos[None].copy(), qvel=qvel[None].copy(), warm=warm[None].copy(), params=params[None].copy())
+    o.step(base, act[None])
+    eps = ulps * 2.0 ** -23
+    for _ in range(trials):
+        st = dict(params=params[None].copy())
+        for k, x in (("qpos", qpos), ("qvel", qvel), ("warm", warm)):
+            st[k] = (x * (1 + eps * rng.uniform(-1, 1, x.shape)))[None]
+        o.step(st, act[None])
+        _, _, ok = _state_err(st["qpos"], st["qvel"], base["qpos"], base["qvel"])
+        if not ok[0]:
+            return True
+    return False
+
+
+def _classify_misses(env_id, misses, frame_skip, variation=None):
+    """every miss must be a discrete event (_discrete_event: the contact / row set differs, or a
+    contact sits within fp32 rounding of its margin) or a step the fp64 reference itself cannot
+    resolve at fp32 resolution (_fp32_sensitive): returns the unexplained ones"""
+    if not misses:
+        return []
+    o = make_oracle(env_id, variation)[1]
+    out = []
+    for (k, e, params, q, v, w, a) in misses:
+        if _discrete_event(env_id, variation, o, params, q, v, w, a, frame_skip):
+            continue
+        if _fp32_sensitive(o, params, q, v, w, a):
+            continue
+        out.append((k, e))
+    return out
+
+
 def _rewards_close(r, r_ref, check=True):
     """per-env reward agreement: |r - r_ref| <= 1e-3 + 1e-3 |r_ref|.  With check, at least
     REWARD_MIN (99.5 %) of the envs must agree -- the remainder is room for a bonus threshold of
@@ -218,7 +291,7 @@ def test_one_env_step_from_identical_states(env_id):
     _, sim = _sim(env_id, n)
     sim.set_state(_t(st["qpos"]), _t(st["qvel"]), _t(st["warm"]), _t(P))
     rng = np.random.default_rng(5)
-    act = rng.uniform(-1, 1, (n, sim.nu))
+    act = f32(rng.uniform(-1, 1, (n, sim.nu)))
     obs, rew = sim.empty(n, sim.obs_dim), sim.empty(n)
     done, goal = sim.empty(n, dtype=torch.uint8), sim.empty(n, dtype=torch.uint8)
     sim.step(_t(act), obs, rew, done, goal)
@@ -413,23 +486,27 @@ def _teacher_forced(env_id, disableflags, policy=False, steps=40, n=64):
         from conftest import GOLDEN
         from mj_envs_amd.policy import GaussianMLP
         pol = GaussianMLP.from_npz(os.path.join(GOLDEN, f"dapg_{env_id.split('-')[0]}.npz"))
-    oks, rok = [], []
+    oks, rok, eqs, evs, misses = [], [], [], [], []
     ostatus = 0
     for k in range(steps):
         sim.get_state(q, v, w)
         torch.cuda.synchronize()
         st = dict(qpos=q.cpu().numpy().astype(np.float64), qvel=v.cpu().numpy().astype(np.float64),
                   warm=w.cpu().numpy().astype(np.float64), params=np.asarray(P, np.float64))
-        act = pol.mean_np(obs.cpu().numpy()) if pol is not None else rng.uniform(-1, 1, (n, sim.nu))
+        pre = {key: val.copy() for key, val in st.items()}
+        # the action the GPU receives (fp32) is the oracle's action too
+        act = f32(pol.mean_np(obs.cpu().numpy()) if pol is not None else rng.uniform(-1, 1, (n, sim.nu)))
         sim.step(_t(act), obs, rew, done, goal)
         sim.get_state(q, v)
         torch.cuda.synchronize()
         _, r_ref, _, _, ost = o.step(st, act, nthreads=8)
         ostatus |= int(np.bitwise_or.reduce(ost))
-        qg, vg = q.cpu().numpy(), v.cpu().numpy()
-        okq = (np.abs(qg - st["qpos"]) <= 2e-5 + 1e-5 * np.abs(st["qpos"])).all(axis=1)
-        okv = (np.abs(vg - st["qvel"]) <= 5e-3 * (1 + np.abs(st["qvel"]))).all(axis=1)
-        oks.append(okq & okv)
+        eq, ev, ok = _state_err(q.cpu().numpy(), v.cpu().numpy(), st["qpos"], st["qvel"])
+        oks.append(ok)
+        eqs.append(eq)
+        evs.append(ev)
+        misses += [(k, e, pre["params"][e], pre["qpos"][e], pre["qvel"][e], pre["warm"][e], np.asarray(act[e], np.float64))
+                   for e in np.where(~ok)[0]]
         rok.append(_rewards_close(rew.cpu().numpy(), r_ref, check=False))
     frac = np.concatenate(oks).mean()
     rfrac = np.concatenate(rok).mean()
@@ -437,11 +514,16 @@ def _teacher_forced(env_id, disableflags, policy=False, steps=40, n=64):
     if miss_steps.sum():
         top = np.argsort(miss_steps)[::-1][:3]
         print(f"misses per step (top 3): " + ", ".join(f"step {k}: {miss_steps[k]}" for k in top))
-    print(f"teacher-forced {env_id} (disableflags {disableflags:#x}{', DAPG policy' if policy else ''}): "
-          f"{frac:.4f} of {n * steps} (env, step) cases within the state tolerance, rewards {rfrac:.4f}")
+    label = f"teacher-forced {env_id} (disableflags {disableflags:#x}{', DAPG policy' if policy else ''})"
+    print(f"{label}: {frac:.4f} of {n * steps} (env, step) cases within the state tolerance, rewards {rfrac:.4f}")
+    err = _err_report(label, np.concatenate(eqs), np.concatenate(evs), np.concatenate(oks))
+    unexplained = _classify_misses(env_id, misses, sim.frame_skip)
+    print(f"{label}: {len(misses)} misses, not explained by a discrete event: {unexplained}")
     assert not (ostatus & 24), "oracle overflowed MuJoCo's capacities"
     _no_overflow(sim, n)
     assert rfrac >= REWARD_MIN, (env_id, rfrac)
+    assert not unexplained, (env_id, unexplained)
+    _err_gate(err)
     return frac
 
 
@@ -467,30 +549,39 @@ def test_teacher_forced_headline_config_4096_envs():
     done, goal = sim.empty(n, dtype=torch.uint8), sim.empty(n, dtype=torch.uint8)
     q, v, w = sim.empty(n, sim.nq), sim.empty(n, sim.nv), sim.empty(n, sim.nv)
     rng = np.random.default_rng(19)
-    oks, roks = [], []
+    oks, roks, eqs, evs, misses = [], [], [], [], []
     for k in range(steps):
         sim.get_state(q, v, w)
         torch.cuda.synchronize()
         st = dict(qpos=q.cpu().numpy()[idx].astype(np.float64), qvel=v.cpu().numpy()[idx].astype(np.float64),
                   warm=w.cpu().numpy()[idx].astype(np.float64), params=np.asarray(P, np.float64)[idx])
-        act = rng.uniform(-1, 1, (n, sim.nu))
+        pre = {key: val.copy() for key, val in st.items()}
+        act = f32(rng.uniform(-1, 1, (n, sim.nu)))
         sim.step(_t(act), obs, rew, done, goal)
         sim.get_state(q, v)
         torch.cuda.synchronize()
         _, r_ref, _, _, _ = o.step(st, act[idx], nthreads=8)
-        qg, vg = q.cpu().numpy()[idx], v.cpu().numpy()[idx]
-        okq = (np.abs(qg - st["qpos"]) <= 2e-5 + 1e-5 * np.abs(st["qpos"])).all(axis=1)
-        okv = (np.abs(vg - st["qvel"]) <= 5e-3 * (1 + np.abs(st["qvel"]))).all(axis=1)
-        oks.append(okq & okv)
+        eq, ev, okk = _state_err(q.cpu().numpy()[idx], v.cpu().numpy()[idx], st["qpos"], st["qvel"])
+        oks.append(okk)
+        eqs.append(eq)
+        evs.append(ev)
+        misses += [(k, int(idx[j]), pre["params"][j], pre["qpos"][j], pre["qvel"][j], pre["warm"][j],
+                    np.asarray(act[idx[j]], np.float64)) for j in np.where(~okk)[0]]
         roks.append(_rewards_close(rew.cpu().numpy()[idx], r_ref, check=False))
     ok = np.array(oks)
     frac, rfrac = ok.mean(), np.concatenate(roks).mean()
     hi = ok[:, idx >= sim.grid].mean()
-    print(f"headline config (hammer-v0, {n} envs, grid {sim.grid}): {frac:.4f} of {ok.size} sampled (env, step) "
+    label = f"headline config (hammer-v0, {n} envs, grid {sim.grid})"
+    print(f"{label}: {frac:.4f} of {ok.size} sampled (env, step) "
           f"cases within tolerance ({hi:.4f} for the claimed envs >= {sim.grid}), rewards {rfrac:.4f}")
+    err = _err_report(label, np.concatenate(eqs), np.concatenate(evs), ok.reshape(-1))
+    unexplained = _classify_misses(env_id, misses, sim.frame_skip)
+    print(f"{label}: {len(misses)} misses, not explained by a discrete event: {unexplained}")
     _no_overflow(sim, n)
     assert frac >= ONE_STEP_MIN and hi >= ONE_STEP_MIN, (frac, hi)
     assert rfrac >= REWARD_MIN, rfrac
+    assert not unexplained, unexplained
+    _err_gate(err)
 
 
 @pytest.mark.parametrize("variation", ["mass", "pos", "size"])
@@ -513,7 +604,7 @@ def test_hammer_variations_one_step(variation):
     pre = {k: np.array(v, copy=True) for k, v in st.items()}
     obs = sim.empty(n, sim.obs_dim)
     sim.set_state(_t(st["qpos"]), _t(st["qvel"]), _t(st["warm"]), _t(P), obs=obs)
-    act = rng.uniform(-1, 1, (n, sim.nu))
+    act = f32(rng.uniform(-1, 1, (n, sim.nu)))
     rew = sim.empty(n)
     done, goal = sim.empty(n, dtype=torch.uint8), sim.empty(n, dtype=torch.uint8)
     sim.step(_t(act), obs, rew, done, goal)

@@ -65,6 +65,7 @@ def main(env_id="hammer-v0", pol_kind="dapg", steps=80, n=64, max_cases=12, dsbl
                   warm=w.cpu().numpy().astype(np.float64), params=P.copy())
         pre = {kk: vv.copy() for kk, vv in st.items()}
         act = pol.mean_np(obs.cpu().numpy()) if pol is not None else rng.uniform(-1, 1, (n, sim.nu))
+        act = np.asarray(act, np.float32).astype(np.float64)      # the GPU's action is the oracle's
         sim.step(t(act), obs, rew, done, goal)
         sim.get_state(q, v)
         torch.cuda.synchronize()
@@ -108,7 +109,8 @@ def main(env_id="hammer-v0", pol_kind="dapg", steps=80, n=64, max_cases=12, dsbl
             gcs = sorted((gname(m, pg[p][0]) + "|" + gname(m, pg[p][1]), round(float(dd), 6))
                          for p, dd in zip(d["con_pair"], d["con_dist"]))
             sub = dict(j=j, rel_qacc=rq, ncon=(d["ncon"], int(sc[0])), nefc=(d["nefc"], int(sc[1])),
-                       newton=(d["solver_iter"], int(sc[2])), noslip=(d["noslip_iter"], int(sc[3])),
+                       newton=(d["solver_iter"], int(sc[2])), newton_exit=d.get("solver_exit"),
+                       noslip=(d["noslip_iter"], int(sc[3])),
                        status=d["status"])
             if d["nefc"] != int(sc[1]):
                 ot, oi, op = o.get("efc_type").astype(int), o.get("efc_id").astype(int), o.get("efc_pos")
