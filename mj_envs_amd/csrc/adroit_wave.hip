@@ -94,34 +94,49 @@ AW_DEV void sort_contacts(Env& s, int lane) {
   wsync();
 }
 
+// Midphase of collider class C (2, 3, 4), lane per pair: a pair whose geoms provably stay farther
+// apart than margin + 1e-4 (aw_collide.h *_may_touch: exact lower bounds on the distance) emits
+// nothing in its collider either and is dropped; the survivors are compacted in place at the
+// front of the class's slice of the list.  Returns their count.
+template <int C>
+AW_DEV int midphase(const DModel& m, Env& s, short* list, int cnt, int lane) {
+  int nsurv = 0;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (int base = 0; base < cnt; base += 64) {
+    const int i = base + lane;
+    const int pair = i < cnt ? list[i] : 0;
+    bool keep = false;
+    if (i < cnt) {
+      if constexpr (C == 2) keep = capbox_may_touch(m, s, pair);
+      else if constexpr (C == 3) keep = boxbox_may_touch(m, s, pair);
+      else keep = mpr_may_touch(m, s, pair);
+    }
+    const unsigned long long mask = __ballot(keep);
+    wsync();
+    if (keep) list[nsurv + __popcll(mask & below)] = (short)pair;
+    nsurv += __popcll(mask);
+    wsync();
+  }
+  return nsurv;
+}
+
 // narrowphase over the broadphase survivors of one collider class
 template <int C>
 AW_DEV void narrow_class(const DModel& m, Env& s, const short* plist, int cnt, int lane) {
   const int st = m.cls_start[C];
   if constexpr (C == 2) {
-    // sphere / capsule - box.  (1) lane per pair: a pair whose segment cannot come within the
-    // margin of the box -- the box's signed distance at the segment centre, less the half-length
-    // and radius, exceeds margin + 1e-4 (the distance is 1-Lipschitz along the segment) -- emits
-    // nothing in the full collider either and is dropped; the survivors are compacted in place.
-    // (2) one survivor per 16-lane DPP row, four per round (capsule-box's 43-candidate minimiser
-    // search is spread over the row, aw_collide.h capbox_tstar_row).
+    // sphere / capsule - box: midphase, then one survivor per 16-lane DPP row, four per round
+    // (capsule-box's 43-candidate minimiser search is spread over the row, capbox_tstar_row)
     short* list = const_cast<short*>(plist) + st;
-    int nsurv = 0;
-    const unsigned long long below = (1ull << lane) - 1ull;
-    for (int base = 0; base < cnt; base += 64) {
-      const int i = base + lane;
-      const int pair = i < cnt ? list[i] : 0;
-      const bool keep = i < cnt && capbox_may_touch(m, s, pair);
-      const unsigned long long mask = __ballot(keep);
-      wsync();
-      if (keep) list[nsurv + __popcll(mask & below)] = (short)pair;
-      nsurv += __popcll(mask);
-      wsync();
-    }
+    const int nsurv = midphase<C>(m, s, list, cnt, lane);
     for (int i0 = 0; i0 < nsurv; i0 += 4) {
       const int i = i0 + (lane >> 4);
       if (i < nsurv) collide_pair<C>(m, s, list[i], lane & 15);
     }
+  } else if constexpr (C == 3) {
+    short* list = const_cast<short*>(plist) + st;
+    const int nsurv = midphase<C>(m, s, list, cnt, lane);
+    for (int i = lane; i < nsurv; i += 64) collide_pair<C>(m, s, list[i]);
   } else {
     for (int i = lane; i < cnt; i += 64) collide_pair<C>(m, s, plist[st + i]);
   }
@@ -141,20 +156,38 @@ AW_DEV void stage_collision(const DModel& m, Env& s, int lane) {
 #pragma unroll
     for (int c = 0; c < NCLASS; c++) cnt[c] = 0;
     const unsigned long long below = (1ull << lane) - 1ull;
-    for (int base = 0; base < m.npairall; base += 64) {   // rounds of 64 pairs
-      const int p = base + lane;
+    // every round's pair data is loaded up front: one model-load latency for the whole list
+    constexpr int NRND = (MAXPAIR + 63) / 64;
+    const int npa = m.npairall;
+    int pkr[NRND];
+    float rbr[NRND];
+#pragma unroll
+    for (int r = 0; r < NRND; r++) {
+      const int p = 64 * r + lane;
+      pkr[r] = p < npa ? MD(cp_pack, p) : 0;
+      rbr[r] = p < npa ? MD(cp_rb, p) : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < NRND; r++) {   // rounds of 64 pairs
+      if (64 * r >= npa) break;
+      const int p = 64 * r + lane;
       bool pass = false;
       int cls = -1;
-      if (p < m.npairall) {
-        const int pk = MD(cp_pack, p);
-        const float rb = MD(cp_rb, p);
+      if (p < npa) {
+        const int pk = pkr[r];
+        const float rb = rbr[r];
         cls = pk & 0xff;
+        const int g1 = (pk >> 8) & 0xff, g2 = pk >> 16;
+        float dif[3];
+        sub3(dif, s.gxpos[g2], s.gxpos[g1]);
         if (rb < 0.f) {
-          pass = true;
+          // plane (g1) pair: the other geom's bounding sphere against the plane through the plane
+          // geom's centre, normal = its z axis (every plane collider emits only within the margin)
+          const float* q = s.gxquat[g1];
+          const float n[3] = {2.f * (q[1] * q[3] + q[0] * q[2]), 2.f * (q[2] * q[3] - q[0] * q[1]),
+                              1.f - 2.f * (q[1] * q[1] + q[2] * q[2])};
+          pass = !(dot3(n, dif) > -rb - 1.f + 1e-4f);
         } else {
-          const int g1 = (pk >> 8) & 0xff, g2 = pk >> 16;
-          float dif[3];
-          sub3(dif, s.gxpos[g1], s.gxpos[g2]);
           pass = !(dot3(dif, dif) > rb * rb);
         }
       }
@@ -176,6 +209,10 @@ AW_DEV void stage_collision(const DModel& m, Env& s, int lane) {
     AW_PROF(s, PR_CO_C2);
     narrow_class<3>(m, s, plist, cnt[3], lane);
     AW_PROF(s, PR_CO_C3);
+    // MPR (cylinder) pairs: the midphase first (fp32 frames, exact distance lower bounds), so
+    // that only pairs that can touch request fp64 frames and run fp64 MPR (hammer: the upright
+    // wall's bounding sphere covers the scene, 5 of its 6 broadphase survivors never touch)
+    if (cnt[4] > 0) cnt[4] = midphase<4>(m, s, plist + m.cls_start[4], cnt[4], lane);
     if (cnt[4] > 0) {
       // the surviving MPR pairs' body closures: only those frames are computed in fp64
       if (lane == 0) s.kin64_mask = 0ull;
@@ -233,7 +270,7 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[Tree<TASK>:
     d.qfrc_con = 0.f;
   } else {
     float a = 0.f;
-    solve_newton<NV, Tree<TASK>::SPLIT>(m, s, lane, Mrow, a, d.qfrc_smooth, d.qacc_smooth);
+    solve_newton<NV>(m, s, lane, Mrow, a, d.qfrc_smooth, d.qacc_smooth);
     AW_PROF(s, PR_NEWTON);
     if (m.noslip_iterations > 0 && !(m.disableflags & DSBL_NOSLIP)) solve_noslip<TASK, KEEP_D>(m, s, lane, Mrow, a);
     AW_PROF(s, PR_NOSLIP);
@@ -1005,7 +1042,9 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
       else c = 1;
       pcls[p] = c;
       ccount[c]++;
-      prb[p] = lo == GEOM_PLANE ? -1.f : (float)((double)crb[a] + (double)crb[b] + (double)pmg[p]);
+      // plane pairs: -(1 + rbound of the other geom + margin) (< -1: the broadphase's plane test)
+      prb[p] = lo == GEOM_PLANE ? (float)(-1.0 - (double)crb[ta == GEOM_PLANE ? b : a] - (double)pmg[p])
+                                : (float)((double)crb[a] + (double)crb[b] + (double)pmg[p]);
     }
     m.cls_start[0] = 0;
     for (int c = 0; c < NCLASS; c++) m.cls_start[c + 1] = m.cls_start[c] + ccount[c];

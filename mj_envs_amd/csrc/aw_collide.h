@@ -861,6 +861,60 @@ AW_DEV bool capbox_may_touch(const DModel& m, const Env& s, int pair) {
   return !(lb > MD(cp_margin, pair) + 1e-4f);
 }
 
+// Conservative midphase of a box - box pair (class 3): false only when the first box's bounding
+// sphere stays farther than the margin from the second box.
+AW_DEV bool boxbox_may_touch(const DModel& m, const Env& s, int pair) {
+  const int g1 = MD(cp_g1, pair), g2 = MD(cp_g2, pair);
+  float mat[9], q[4], dif[3], c[3];
+  for (int k = 0; k < 4; k++) q[k] = s.gxquat[g2][k];
+  q2m(mat, q);
+  sub3(dif, s.gxpos[g1], s.gxpos[g2]);
+  mulmtv3(c, mat, dif);
+  const float zero[3] = {0.f, 0.f, 0.f};
+  const float lb = seg_box_f(c, zero, s.gsize[g2], 0.f) - norm3(s.gsize[g1]);   // box 1's circumradius
+  return !(lb > MD(cp_margin, pair) + 1e-4f);
+}
+
+// Conservative midphase of an MPR (cylinder) pair (class 4), on the fp32 frames: false only when
+// the geoms provably stay farther apart than the margin.  A cylinder lies inside the capsule of
+// its axis segment and radius, so with a box (always the second geom of its pair) the bound is
+// the box's signed distance at the first geom's centre less its circumradius; otherwise the
+// distance of the two axis segments less both radii (sphere: a point).
+AW_DEV bool mpr_may_touch(const DModel& m, const Env& s, int pair) {
+  const int g1 = MD(cp_g1, pair), g2 = MD(cp_g2, pair);
+  const int t1 = MD(geom_type, g1), t2 = MD(geom_type, g2);
+  const float* z1 = s.gsize[g1];
+  const float h1 = t1 == GEOM_SPHERE ? 0.f : z1[1];
+  float lb;
+  if (t2 == GEOM_BOX) {
+    float mat[9], q[4], dif[3], c[3];
+    for (int k = 0; k < 4; k++) q[k] = s.gxquat[g2][k];
+    q2m(mat, q);
+    sub3(dif, s.gxpos[g1], s.gxpos[g2]);
+    mulmtv3(c, mat, dif);
+    const float zero[3] = {0.f, 0.f, 0.f};
+    const float circ = t1 == GEOM_CYLINDER ? sqrtf(z1[0] * z1[0] + h1 * h1) : z1[0] + h1;
+    lb = seg_box_f(c, zero, s.gsize[g2], 0.f) - circ;
+  } else {
+    const float* z2 = s.gsize[g2];
+    const float h2 = t2 == GEOM_SPHERE ? 0.f : z2[1];
+    float q1[4], q2[4], m1[9], m2[9];
+    for (int k = 0; k < 4; k++) { q1[k] = s.gxquat[g1][k]; q2[k] = s.gxquat[g2][k]; }
+    q2m(m1, q1);
+    q2m(m2, q2);
+    float s1[3], d1[3], s2[3], d2[3], c1[3], c2[3];
+    for (int k = 0; k < 3; k++) {
+      s1[k] = s.gxpos[g1][k] - m1[3 * k + 2] * h1; d1[k] = 2.f * m1[3 * k + 2] * h1;
+      s2[k] = s.gxpos[g2][k] - m2[3 * k + 2] * h2; d2[k] = 2.f * m2[3 * k + 2] * h2;
+    }
+    seg_seg(s1, d1, s2, d2, c1, c2);
+    float dd[3];
+    sub3(dd, c1, c2);
+    lb = norm3(dd) - z1[0] - z2[0];
+  }
+  return !(lb > MD(cp_margin, pair) + 1e-4f);
+}
+
 // ---------------------------------------------------------------------------------------
 // narrowphase of one pair of collider class C (host: adroit_wave.hip build_model pcls):
 // 0 plane-*, 1 sphere/capsule pairs, 2 sphere/capsule-box, 3 box-box, 4 anything with a

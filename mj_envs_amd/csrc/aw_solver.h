@@ -66,77 +66,6 @@ AW_DEV void chol_factor(float (&row)[NV], int lane_in, float& invd, Env& s) {
     }
   }
 }
-// Block-split LDL': when no lower-triangle entry couples the hand block [0, P) with the object
-// block [P, NV) (M is block-diagonal across the dof trees; J'DJ couples them only through a
-// hand-object contact), column j of the hand block and column P + j of the object block are
-// pivoted in the same step, so the serial chain is P columns instead of NV.  Lane i's multiplier
-// is its own entry of its block's current column; updates of a lane's cross-block entries are
-// garbage and are zeroed at the end, updates of an object lane's already-pivoted columns are
-// masked (coefficient 0).  In the decoupled case every operand of the plain factor's fma chain
-// is the same (a cross term enters it as fma(-a, 0, x) = x), so the factor is bitwise the plain
-// one's.
-template <int NV, int P>
-AW_DEV void chol_factor_split(float (&row)[NV], int lane_in, float& invd, Env& s) {
-  constexpr int NB = NV - P, LA = AW_CHOL_LA;
-  static_assert(NB > 0 && NB + LA <= P, "object block must finish before the hand block's look-ahead tail");
-  const int lane = opaque(lane_in);
-  const bool inA = lane < P;
-  float* col = reinterpret_cast<float*>(s.colbuf);
-#pragma unroll
-  for (int j = 0; j < P; j++) {
-    const bool hasB = j < NB;
-    const int jb = hasB ? P + j : P;                 // object column of this step (clamped when done)
-    const float dA = rlane(row[j], j);
-    const float dB = hasB ? rlane(row[jb], jb) : dA;
-    const float dj = __builtin_amdgcn_fmed3f(inA ? dA : dB, MINVAL, 3.402823466e38f);
-    const float inv = __builtin_amdgcn_rcpf(dj);
-    const float a = inA ? row[j] : (hasB ? row[jb] : 0.f);
-    const float aA = inA ? a : 0.f;
-    const int pl = inA ? j : (hasB ? jb : 64);
-    if (lane == pl) invd = inv;
-    const float u = lane > pl ? a * inv : 0.f;
-    if (hasB) {
-      row[j] = inA ? u : row[j];
-      row[jb] = inA ? row[jb] : u;
-    } else {
-      row[j] = u;
-    }
-    // coefficient for column k at this step: an object lane's columns [P, P + j] are pivoted
-    auto coef = [&](int k) { return (k >= P && k <= P + j) ? aA : a; };
-    auto in_la = [&](int k) {
-      return (k > j && k <= j + LA) || (hasB && k > jb && k <= jb + LA);
-    };
-#pragma unroll
-    for (int t = 1; t <= LA; t++) {
-      if (j + t < NV) row[j + t] = fmaf(-coef(j + t), rlane(u, j + t), row[j + t]);
-      if (hasB && jb + t < NV) row[jb + t] = fmaf(-coef(jb + t), rlane(u, jb + t), row[jb + t]);
-    }
-    bool any = false;
-#pragma unroll
-    for (int k = j + 1; k < NV; k++) any = any || !in_la(k);
-    if (any) {
-      col[lane] = u;
-      wsync();
-#pragma unroll
-      for (int q = (j + 1) >> 2; q <= (NV - 1) >> 2; q++) {
-        bool need = false;
-#pragma unroll
-        for (int t = 0; t < 4; t++) need = need || (4 * q + t > j && 4 * q + t < NV && !in_la(4 * q + t));
-        if (!need) continue;
-        const float4 c = s.colbuf[q];
-        const float cv[4] = {c.x, c.y, c.z, c.w};
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-          const int k = 4 * q + t;
-          if (k > j && k < NV && !in_la(k)) row[k] = fmaf(-coef(k), cv[t], row[k]);
-        }
-      }
-      wsync();
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < NV; k++) row[k] = (k < P) == inA ? row[k] : 0.f;
-}
 // packed rows of U into s.L (row padding included: the factor-reuse path reloads whole 4-blocks)
 template <int NV>
 AW_DEV void chol_store(const float (&row)[NV], int lane_in, Env& s) {
@@ -238,9 +167,36 @@ AW_DEV float row_dot(const DModel& m, const Env& s, int r, const float* x) {
   return acc;
 }
 
-// out_k = (J' f)_k for k = lane; f given per row in s.rowbuf (must be written + synced)
+// (J_r . x, J_r . y) for two vectors in LDS: one pass over the row's entries
 template <int NV>
-AW_DEV float jt_mul(const DModel& m, Env& s, int lane) {
+AW_DEV void row_dot2(const DModel& m, const Env& s, int r, const float* x, const float* y, float& dx, float& dy) {
+  if (r < s.nsparse) {
+    const int i0 = s.efc_i0[r], i1 = s.efc_i1[r];
+    const float v0 = s.efc_v0[r], v1 = s.efc_v1[r];
+    dx = v0 * x[i0] + (i1 >= 0 ? v1 * x[i1] : 0.f);
+    dy = v0 * y[i0] + (i1 >= 0 ? v1 * y[i1] : 0.f);
+    return;
+  }
+  const int d = r - s.nsparse;
+  float ax = 0.f, ay = 0.f;
+  if (d < JL) {
+    const float* J = s.J[d];
+#pragma unroll
+    for (int k = 0; k < NV; k++) { ax = fmaf(J[k], x[k], ax); ay = fmaf(J[k], y[k], ay); }
+  } else {
+    gp_t<const float> J = jspill_row(m, s, d);
+#pragma unroll
+    for (int k = 0; k < NV; k++) { const float j = J[k]; ax = fmaf(j, x[k], ax); ay = fmaf(j, y[k], ay); }
+  }
+  dx = ax;
+  dy = ay;
+}
+
+// out_k = (J' f)_k for k = lane; f given per row in s.rowbuf (must be written + synced)
+// ABS: *absum = the lane's sum of the magnitudes of its terms (|sparse part| + sum_d |J_dk f_d|),
+// the scale of the result's fp32 rounding noise
+template <int NV, bool ABS = false>
+AW_DEV float jt_mul(const DModel& m, Env& s, int lane, float* absum = nullptr) {
   if (lane < NV) s.vec2[lane] = 0.f;
   wsync();
   for (int r = lane; r < s.nsparse; r += 64) {
@@ -254,6 +210,7 @@ AW_DEV float jt_mul(const DModel& m, Env& s, int lane) {
   wsync();
   const int li = lane < NV ? lane : NV - 1;
   float out = s.vec2[li];
+  float oa = fabsf(out);
   const int nd = s.ndense, ndl = nd < JL ? nd : JL;
   // unrolled by 4: the loads of four rows are issued before their fmas (one load latency per
   // four rows, not per row; the spill rows are global loads)
@@ -261,12 +218,21 @@ AW_DEV float jt_mul(const DModel& m, Env& s, int lane) {
 #define AW_JT_UNROLL 4
 #endif
 #pragma unroll AW_JT_UNROLL
-  for (int d = 0; d < ndl; d++) out = fmaf(s.J[d][li], s.rowbuf[s.nsparse + d], out);
+  for (int d = 0; d < ndl; d++) {
+    const float j = s.J[d][li], f = s.rowbuf[s.nsparse + d];
+    out = fmaf(j, f, out);
+    if (ABS) oa = fmaf(fabsf(j), fabsf(f), oa);
+  }
   if (nd > JL) {
     gp_t<const float> Jg = jspill_row(m, s, JL);
 #pragma unroll AW_JT_UNROLL
-    for (int d = JL; d < nd; d++) out = fmaf(Jg[(d - JL) * VS + li], s.rowbuf[s.nsparse + d], out);
+    for (int d = JL; d < nd; d++) {
+      const float j = Jg[(d - JL) * VS + li], f = s.rowbuf[s.nsparse + d];
+      out = fmaf(j, f, out);
+      if (ABS) oa = fmaf(fabsf(j), fabsf(f), oa);
+    }
   }
+  if (ABS) *absum = lane < NV ? oa : 0.f;
   return lane < NV ? out : 0.f;
 }
 
@@ -472,16 +438,16 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
 
 // ---------------------------------------------------------------------------------------
 // Newton solver
-constexpr float GRAD_NOISE = 2e-6f;   // ~16 fp32 ulps of the gradient's terms
-#ifndef AW_NT_NOISE
-#define AW_NT_NOISE 0
-#endif
+// fp32 termination of the Newton solve, per dof: a gradient component below this fraction of the
+// summed magnitudes of its terms (sum_k |M_ik a_k|, |qfrc_smooth_i|, sum_r |J_ri f_r|) is rounding
+// noise.  Per dof, not over the norm of all dofs: a light object's dofs (relocate's ball) are not
+// masked by the hand's large forces (the norm-wide floor stopped one iteration before the fp64
+// reference on relocate's first steps, r04c); and over the terms' magnitudes, not the sums' (with
+// |Ma_i| etc. a component whose terms cancel never reached its floor: 20-iteration solves, r04h).
 #ifndef AW_NT_NOISE_DOF
-#define AW_NT_NOISE_DOF 2e-6f
+#define AW_NT_NOISE_DOF 4e-6f
 #endif
-#ifndef AW_NT_IMPROVE
-#define AW_NT_IMPROVE 0
-#endif
+constexpr float NT_NOISE_DOF = AW_NT_NOISE_DOF;
 // why the Newton solve stopped (s.it_newton = iterations + 1000 * reason, aw_forward_dump)
 enum { NT_EXIT_MAXITER = 0, NT_EXIT_NOSTEP = 1, NT_EXIT_NOISE = 2, NT_EXIT_IMPROVE = 3, NT_EXIT_GRAD = 4 };
 #ifndef AW_NSP_CACHE
@@ -588,7 +554,7 @@ AW_DEV void hess_dense_mfma(const DModel& m, Env& s, int lane) {
   }
 }
 
-template <int NV, int SPLIT = 0>
+template <int NV>
 AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mrow)[NV], float& a, float qfrc_smooth,
                          float qacc_smooth) {
   const int lane = lane_nt;
@@ -610,41 +576,71 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
   }
   const float scale = 1.f / (m.meaninertia * (float)(NV > 1 ? NV : 1));
   float Ma;
-  auto set_point = [&](float x) {
-    a = lane < NV ? x : 0.f;
-    if (lane < NV) s.vec[lane] = a;
+  // both starting points (qacc_smooth, warmstart) in one pass over M and the rows, then the
+  // cheaper one is kept (mj_solNewton: the warmstart when its cost is strictly lower); r04h A/B
+  // against two set-point passes: -0.6 % random, -1.0 % DAPG
+  float cost;
+  {
+    const bool ws = !(m.disableflags & DSBL_WARMSTART);
+    const float aw = ws && lane < NV ? s.warm[lane] : 0.f;
+    if (lane < NV) { s.vec[lane] = a0; s.vec2[lane] = aw; }
     wsync();
-    Ma = matvec_lds<NV>(Mrow, s.vec);
+    const float Ma0 = matvec_lds<NV>(Mrow, s.vec);
+    const float Maw = matvec_lds<NV>(Mrow, s.vec2);
+    float j0[NRL], jw[NRL];
 #pragma unroll
     for (int h = 0; h < NRL; h++) {
-      int r = lane + 64 * h;
-      if (r < nefc) rr[h].Jaref = row_dot<NV>(m, s, r, s.vec) - s.efc_aref[r];
+      const int r = lane + 64 * h;
+      j0[h] = jw[h] = 0.f;
+      if (r < nefc) {
+        row_dot2<NV>(m, s, r, s.vec, s.vec2, j0[h], jw[h]);
+        const float ar = s.efc_aref[r];
+        j0[h] -= ar;
+        jw[h] -= ar;
+      }
     }
     wsync();
-  };
-  auto eval = [&]() {
-    float g = lane < NV ? (Ma - fs) * (a - a0) : 0.f;
-    float c = 0.f;
+    float c0 = 0.f, cwl = 0.f, fw[NRL];
+    int sw[NRL];
 #pragma unroll
-    for (int h = 0; h < NRL; h++) c += row_eval(rr[h], rr[h].Jaref, &rr[h].force, &rr[h].st);
-    return 0.5f * wave_sum(g) + wave_sum(c);
-  };
-  set_point(a0);
-  float cost = eval();
-  if (!(m.disableflags & DSBL_WARMSTART)) {
-    float aw = lane < NV ? s.warm[lane] : 0.f;
-    set_point(aw);
-    float cw = eval();
-    if (cw < cost) cost = cw;
-    else { set_point(a0); cost = eval(); }
+    for (int h = 0; h < NRL; h++) {
+      c0 += row_eval(rr[h], j0[h], &rr[h].force, &rr[h].st);
+      cwl += row_eval(rr[h], jw[h], &fw[h], &sw[h]);
+    }
+    cost = wave_sum(c0);   // the Gauss term is 0 at qacc_smooth
+    const float cw = ws ? 0.5f * wave_sum(lane < NV ? (Maw - fs) * (aw - a0) : 0.f) + wave_sum(cwl) : cost;
+    const bool take_w = ws && cw < cost;
+    cost = take_w ? cw : cost;
+    a = take_w ? aw : (lane < NV ? a0 : 0.f);
+    Ma = take_w ? Maw : Ma0;
+#pragma unroll
+    for (int h = 0; h < NRL; h++) {
+      rr[h].Jaref = take_w ? jw[h] : j0[h];
+      rr[h].force = take_w ? fw[h] : rr[h].force;
+      rr[h].st = take_w ? sw[h] : rr[h].st;
+    }
   }
-  float gref = 0.f;   // |Ma|^2 + |fs|^2 + |J'f|^2 per lane: the fp32 noise scale of the gradient
+  // fp32 noise scale of each gradient component Ma_i - fs_i - (J'f)_i: the magnitudes of all of
+  // its terms, sum_k |M_ik a_k| + |fs_i| + sum_r |J_ri f_r| (the magnitude of a sum would miss the
+  // cancellation inside it)
+  float gnoise = 0.f;
   auto gradient = [&]() {
 #pragma unroll
     for (int h = 0; h < NRL; h++) { int r = lane + 64 * h; if (r < nefc) s.rowbuf[r] = rr[h].force; }
+    if (lane < NV) s.hdiag[lane] = fabsf(a);
     wsync();
-    float jf = jt_mul<NV>(m, s, lane);
-    gref = lane < NV ? Ma * Ma + fs * fs + jf * jf : 0.f;
+    float jfa;
+    float jf = jt_mul<NV, true>(m, s, lane, &jfa);
+    float maa = 0.f;
+#pragma unroll
+    for (int q = 0; q < (NV + 3) / 4; q++) {
+      const float4 v = *reinterpret_cast<const float4*>(s.hdiag + 4 * q);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+        if (4 * q + t < NV) maa = fmaf(fabsf(Mrow[4 * q + t]), vv[t], maa);
+    }
+    gnoise = lane < NV ? maa + fabsf(fs) + jfa : 0.f;
     return lane < NV ? Ma - fs - jf : 0.f;
   };
   float grad = gradient();
@@ -787,7 +783,6 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
     }
     AW_PROF(s, PR_NT_LS);
     if (alpha == 0.f) { iter++; why = NT_EXIT_NOSTEP; break; }
-#if AW_NT_IMPROVE
     // the rows' cost before the step, per lane (the improvement below is formed from per-row
     // differences, not as the difference of two whole costs)
     float rc_old = 0.f;
@@ -797,43 +792,27 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
       int st;
       rc_old += row_eval(rr[h], rr[h].Jaref, &f, &st);
     }
-#endif
     a += alpha * p;
     Ma += alpha * Mp;
 #pragma unroll
     for (int h = 0; h < NRL; h++) rr[h].Jaref += alpha * rr[h].Jp;
-    float oldcost = cost;
-#if AW_NT_IMPROVE
     // mj_solNewton's improvement = scale (oldcost - cost) without the fp32 cancellation of two
     // whole costs: the smooth part's change along the line is exactly alpha c0 + alpha^2 c1 / 2
-    // (M a0 = qfrc_smooth, so p' M (a - a0) = c0), the rows' change is summed row by row
+    // (M a0 = qfrc_smooth, so p' M (a - a0) = c0), the rows' change is summed row by row.  (The
+    // difference of the two fp32 costs carried their rounding noise, ~1e-7 of the cost: r04f/g
+    // A/B, C3 hammer 8 -> 0 misses.)
     float rc_new = 0.f;
 #pragma unroll
     for (int h = 0; h < NRL; h++) rc_new += row_eval(rr[h], rr[h].Jaref, &rr[h].force, &rr[h].st);
-    cost = oldcost + alpha * c0 + 0.5f * alpha * alpha * c1 + wave_sum(rc_new - rc_old);
     const float dcost = -(alpha * c0 + 0.5f * alpha * alpha * c1 + wave_sum(rc_new - rc_old));
-#else
-    cost = eval();
-#endif
     grad = gradient();
     float gn = sqrtf(wave_sum(grad * grad));
-#if AW_NT_IMPROVE
     float improvement = scale * dcost, gradnorm = scale * gn;
-#else
-    float improvement = scale * (oldcost - cost), gradnorm = scale * gn;
-#endif
-    // fp32 termination: a gradient at the rounding floor of its own terms (Ma, qfrc_smooth,
-    // J'f) cannot shrink further -- the fp64 reference would already stop on its 1e-8 test
-    // here; an extra Newton step in fp32 only re-solves the same active set.
-#if AW_NT_NOISE == 1
-    // per dof: every component at the floor of its OWN terms (a light object's dofs are not
-    // masked by the hand's large forces, as a norm over all dofs would let them be)
-    if (__ballot(lane < NV && fabsf(grad) > AW_NT_NOISE_DOF * sqrtf(gref)) == 0ull) { iter++; why = NT_EXIT_NOISE; break; }
-#elif AW_NT_NOISE == 2
-    // no noise-floor exit: MuJoCo's own improvement / gradient tests only
-#else
-    if (gn <= GRAD_NOISE * sqrtf(wave_sum(gref))) { iter++; why = NT_EXIT_NOISE; break; }
-#endif
+    // fp32 termination: every gradient component at the rounding floor of its own terms (Ma,
+    // qfrc_smooth, J'f) cannot shrink further -- the fp64 reference would already stop on its
+    // 1e-8 test here; an extra Newton step in fp32 only re-solves the same active set.  (Without
+    // this exit: +8 % k_step, r04g.)
+    if (__ballot(lane < NV && fabsf(grad) > NT_NOISE_DOF * gnoise) == 0ull) { iter++; why = NT_EXIT_NOISE; break; }
     AW_PROF(s, PR_NT_UPD);
     if (improvement < m.tolerance) { iter++; why = NT_EXIT_IMPROVE; break; }
     if (gradnorm < m.tolerance) { iter++; why = NT_EXIT_GRAD; break; }

@@ -170,22 +170,48 @@ def _err_gate(r):
         assert r[k][1] <= ERR_P99[k], (k, "p99", r[k][1])
 
 
-def _fp32_sensitive(o, params, qpos, qvel, warm, act, trials=8, ulps=4, seed=0):
+_ORACLE_F32MODEL = {}
+
+
+def _oracle_f32_model(env_id, variation=None):
+    """The fp64 oracle on the model the GPU holds: every floating-point model constant rounded to
+    fp32 (the kernel's model table is fp32)."""
+    key = (env_id, variation)
+    if key not in _ORACLE_F32MODEL:
+        from mj_envs_amd.tasks import attach_task, load_model
+        from oracle.pyoracle import Oracle
+        m = attach_task(load_model(env_id), env_id, variation)
+        for k, v in list(m.arrays.items()):
+            a = np.asarray(v)
+            if a.dtype.kind == "f":
+                m.arrays[k] = a.astype(np.float32).astype(np.float64)
+        m.opt = {k: (float(np.float32(v)) if isinstance(v, float) else v) for k, v in m.opt.items()}
+        _ORACLE_F32MODEL[key] = Oracle(m.to_blob())
+    return _ORACLE_F32MODEL[key]
+
+
+def _fp32_sensitive(o, params, qpos, qvel, warm, act, env_id=None, variation=None, trials=8, ulps=8, seed=0):
     """Is the fp64 reference itself unstable at fp32 resolution here?  Re-runs the oracle's
-    env-step from the same state with every state component perturbed by up to `ulps` fp32 ulps
-    (relative 2^-23 each): True when some perturbed result leaves the one-step tolerance around
-    the unperturbed one -- the step sits on a discontinuity (a contact, row state or solver
-    decision switching) or is ill-conditioned within fp32 rounding of its input, so an fp32
-    simulation cannot be held to it."""
+    env-step (a) on the fp32-rounded model the GPU holds and (b) from the same state with every
+    state component perturbed by up to `ulps` fp32 ulps (relative 2^-23 each): True when one of
+    those results leaves the one-step tolerance around the unperturbed fp64 one -- the step sits
+    on a discontinuity (a contact, row state or solver decision switching) or is ill-conditioned
+    within fp32 rounding of its inputs, so an fp32 simulation cannot be held to it."""
     rng = np.random.default_rng(seed)
     base = dict(qpos=qpos[None].copy(), qvel=qvel[None].copy(), warm=warm[None].copy(), params=params[None].copy())
     o.step(base, act[None])
+    runs = []
+    if env_id is not None:
+        runs.append((_oracle_f32_model(env_id, variation), dict(qpos=qpos[None].copy(), qvel=qvel[None].copy(),
+                                                               warm=warm[None].copy(), params=params[None].copy())))
     eps = ulps * 2.0 ** -23
     for _ in range(trials):
         st = dict(params=params[None].copy())
         for k, x in (("qpos", qpos), ("qvel", qvel), ("warm", warm)):
             st[k] = (x * (1 + eps * rng.uniform(-1, 1, x.shape)))[None]
-        o.step(st, act[None])
+        runs.append((o, st))
+    for oo, st in runs:
+        oo.step(st, act[None])
         _, _, ok = _state_err(st["qpos"], st["qvel"], base["qpos"], base["qvel"])
         if not ok[0]:
             return True
@@ -203,7 +229,7 @@ def _classify_misses(env_id, misses, frame_skip, variation=None):
     for (k, e, params, q, v, w, a) in misses:
         if _discrete_event(env_id, variation, o, params, q, v, w, a, frame_skip):
             continue
-        if _fp32_sensitive(o, params, q, v, w, a):
+        if _fp32_sensitive(o, params, q, v, w, a, env_id, variation):
             continue
         out.append((k, e))
     return out
