@@ -156,26 +156,13 @@ AW_DEV void stage_collision(const DModel& m, Env& s, int lane) {
 #pragma unroll
     for (int c = 0; c < NCLASS; c++) cnt[c] = 0;
     const unsigned long long below = (1ull << lane) - 1ull;
-    // every round's pair data is loaded up front: one model-load latency for the whole list
-    constexpr int NRND = (MAXPAIR + 63) / 64;
-    const int npa = m.npairall;
-    int pkr[NRND];
-    float rbr[NRND];
-#pragma unroll
-    for (int r = 0; r < NRND; r++) {
-      const int p = 64 * r + lane;
-      pkr[r] = p < npa ? MD(cp_pack, p) : 0;
-      rbr[r] = p < npa ? MD(cp_rb, p) : 0.f;
-    }
-#pragma unroll
-    for (int r = 0; r < NRND; r++) {   // rounds of 64 pairs
-      if (64 * r >= npa) break;
-      const int p = 64 * r + lane;
+    for (int base = 0; base < m.npairall; base += 64) {   // rounds of 64 pairs
+      const int p = base + lane;
       bool pass = false;
       int cls = -1;
-      if (p < npa) {
-        const int pk = pkr[r];
-        const float rb = rbr[r];
+      if (p < m.npairall) {
+        const int pk = MD(cp_pack, p);
+        const float rb = MD(cp_rb, p);
         cls = pk & 0xff;
         const int g1 = (pk >> 8) & 0xff, g2 = pk >> 16;
         float dif[3];

@@ -344,16 +344,20 @@ AW_DEV float wave_max(float x) {
   x = fmaxf(x, dpp_f<0x143, 0xC>(NEG, x));
   return rlane(x, 63);
 }
-// exclusive prefix sum of small non-negative ints across the wave
+// exclusive prefix sum of small non-negative ints (< 2^BITS) across the wave, bit-sliced: one
+// ballot + popcount per bit (scalar work), no lane shuffles through the LDS crossbar
+template <int BITS>
 AW_DEV int wave_excl_scan(int x, int lane, int* total) {
-  int v = x;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int pre = 0, tot = 0;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int y = __shfl_up(v, o, 64);
-    if (lane >= o) v += y;
+  for (int b = 0; b < BITS; b++) {
+    const unsigned long long mk = __ballot((x >> b) & 1);
+    pre += __popcll(mk & below) << b;
+    tot += __popcll(mk) << b;
   }
-  *total = __shfl(v, 63, 64);
-  return v - x;
+  *total = tot;
+  return pre;
 }
 
 // ---------------------------------------------------------------------------------------

@@ -270,7 +270,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
     dlo = (float)(d0 - mgd); dhi = (float)(d1 - mgd);
   }
   int njl;
-  int off = nfl + wave_excl_scan(lo + hi, lane, &njl);
+  int off = nfl + wave_excl_scan<2>(lo + hi, lane, &njl);
   if (lo || hi) {
     for (int side = 0; side < 2; side++) {
       if (!(side ? hi : lo)) continue;
@@ -295,7 +295,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
     dlo = (float)(e0 - mgd); dhi = (float)(e1 - mgd);
   }
   int ntl;
-  off = nfl + njl + wave_excl_scan(lo + hi, lane, &ntl);
+  off = nfl + njl + wave_excl_scan<2>(lo + hi, lane, &ntl);
   if (lo || hi) {
     for (int side = 0; side < 2; side++) {
       if (!(side ? hi : lo)) continue;
@@ -319,7 +319,8 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
     nr = dim == 1 ? 1 : 2 * (dim - 1);
   }
   int ntot;
-  int doff = wave_excl_scan(nr, lane, &ntot);
+  static_assert(2 * (6 - 1) < 16, "rows per contact (condim <= 6) fit the scan's 4 bits");
+  int doff = wave_excl_scan<4>(nr, lane, &ntot);
   bool inc = lane < ncon && doff + nr <= MAXDENSE && nsparse + doff + nr <= MAXEFC;
   int nd = 0;
   {
