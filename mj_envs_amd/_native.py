@@ -111,11 +111,13 @@ STAGES = ("pre", "kinematics", "collision", "com_crb", "rne_smooth_solve", "cons
 SUBSTAGES = ("nt_init", "nt_hess", "nt_chol", "nt_solve", "nt_ls", "nt_upd", "ns_minv", "ns_setup", "ns_iter",
              "co_broad", "co_narrow", "com", "rne", "co_plane", "co_round", "co_roundbox", "co_boxbox",
              "nt_hsparse", "nt_hoffd")
+# timed intervals recorded in slots past the counters (stage_profile: v[39..41])
+EXTRA_STAGES = ("co_kin64", "cs_sparse", "cs_j")
 
 
 def stage_profile(reset: bool = True) -> dict:
     """Per-stage shader-clock cycles of k_step (diagnostic build only, see aw_stage_profile)."""
-    buf = (ctypes.c_ulonglong * 40)()
+    buf = (ctypes.c_ulonglong * 44)()
     _check(load().aw_stage_profile(buf, int(reset)))
     v = list(buf)
     out = {name: v[i] for i, name in enumerate(STAGES)}
@@ -125,6 +127,7 @@ def stage_profile(reset: bool = True) -> dict:
         out[name] = v[19 + i]
     out["offd_rows"] = v[38]
     out["co_kin64"] = v[39]
+    out["cs_sparse"], out["cs_j"] = v[40], v[41]
     return out
 
 

@@ -573,8 +573,21 @@ template <class T> AW_DEV bool eq(T a, T b) {
   return fb > fa ? ab < EPS_T<T> * fb : ab < EPS_T<T> * fa;
 }
 template <class T> AW_DEV bool veq(const T* a, const T* b) { return eq(a[0], b[0]) && eq(a[1], b[1]) && eq(a[2], b[2]); }
+// 1 / sqrt(x): the hardware estimate refined by Newton steps (fp64: two steps from v_rsq_f64 give
+// full double precision for normal x, where the correctly rounded sqrt + divide expansions cost
+// ~3x the instructions on the MPR's serial chain: -1.4 % k_step, r04m)
+template <class T> AW_DEV T rsqrt_fast(T x) {
+  if constexpr (sizeof(T) == 8) {
+    double r = __builtin_amdgcn_rsq(x);
+    const double hx = 0.5 * x;
+    r = r * fma(-hx * r, r, 1.5);
+    r = r * fma(-hx * r, r, 1.5);
+    return r;
+  }
+  return T(1.0) / sqrt(x);
+}
 template <class T> AW_DEV void vnorm(T* v) {
-  T k = T(1.0) / sqrt(dot3(v, v));
+  T k = rsqrt_fast(dot3(v, v));
   scl3(v, v, k);
 }
 template <class T> AW_DEV T sgn(T x) { return x < 0 ? -T(1.0) : (x > 0 ? T(1.0) : T(0.0)); }
@@ -591,8 +604,8 @@ template <class T> AW_DEV void gsupport(T* res, const GVdT<T>& g, const T* dir, 
   const bool box = g.type == GEOM_BOX, cyl = g.type == GEOM_CYLINDER, cap = g.type == GEOM_CAPSULE;
   const bool round = g.type == GEOM_SPHERE || cap;
   const T sg0 = sgn(ld[0]), sg1 = sgn(ld[1]), sg2 = sgn(ld[2]);
-  const T tmp = sqrt(ld[0] * ld[0] + ld[1] * ld[1]);
-  const T ci = tmp > MINVAL ? s[0] / tmp : T(0.0);
+  const T t2 = ld[0] * ld[0] + ld[1] * ld[1];   // the cylinder's radial direction: |ld_xy| > MINVAL
+  const T ci = t2 > T(MINVAL) * T(MINVAL) ? s[0] * rsqrt_fast(t2) : T(0.0);
   r[0] = box ? sg0 * s[0] : (cyl ? ld[0] * ci : (round ? ld[0] * s[0] : T(0.0)));
   r[1] = box ? sg1 * s[1] : (cyl ? ld[1] * ci : (round ? ld[1] * s[0] : T(0.0)));
   r[2] = box ? sg2 * s[2] : (cyl ? sg2 * s[1] : (round ? fma(ld[2], s[0], cap ? sg2 * s[1] : T(0.0)) : T(0.0)));

@@ -43,16 +43,16 @@ constexpr float MINVAL = 1e-15f;
 
 // Stage profiler (diagnostic builds only, -DAW_STAGE_PROF): shader-clock cycles per stage,
 // summed over waves; read back through aw_stage_profile().
-constexpr int AW_NPROF = 40;
+constexpr int AW_NPROF = 44;
 enum {
   PR_PRE = 0, PR_KIN, PR_COLL, PR_CRB, PR_SMOOTH, PR_CONSTR, PR_NEWTON, PR_NOSLIP, PR_JT_TOUCH,
   PR_EULER, PR_TASK, PR_RESET, PR_CHECK, PR_CALLS, PR_SUBSTEPS,
   PR_NEWTON_IT, PR_NOSLIP_IT, PR_NEFC, PR_NCON,
   PR_NT_INIT, PR_NT_HESS, PR_NT_CHOL, PR_NT_SOLVE, PR_NT_LS, PR_NT_UPD, PR_NS_MINV, PR_NS_SETUP, PR_NS_ITER,
   PR_CO_BROAD, PR_CO_NARROW, PR_COM, PR_RNE, PR_CO_C0, PR_CO_C1, PR_CO_C2, PR_CO_C3,
-  PR_NT_HSPARSE, PR_NT_HOFFD, PR_NT_OFFD_ROWS, PR_CO_KIN64
+  PR_NT_HSPARSE, PR_NT_HOFFD, PR_NT_OFFD_ROWS, PR_CO_KIN64, PR_CS_SPARSE, PR_CS_J
 };
-static_assert(PR_CO_KIN64 < AW_NPROF, "stage profiler ids");
+static_assert(PR_CS_J < AW_NPROF, "stage profiler ids");
 #ifdef AW_STAGE_PROF
 #define AW_PROF_START(S)                                            \
   do {                                                              \

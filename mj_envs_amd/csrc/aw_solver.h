@@ -350,6 +350,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
   }
   if (lane == 0) { s.nsparse = nsparse; s.ndense = nd; s.nefc = nsparse + nd; }
   wsync();
+  AW_PROF(s, PR_CS_SPARSE);
   // dense J rows: one contact at a time, lane = dof.  The per-contact model data is gathered
   // first with lane = contact (one round of loads) and broadcast with readlane in the loop.
   unsigned long long c_m1 = 0ull, c_m2 = 0ull;
@@ -408,6 +409,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
   }
   if (nd > JL) jspill_fence();
   wsync();
+  AW_PROF(s, PR_CS_J);
   // impedance, regularisation, reference acceleration
   for (int r = lane; r < s.nefc; r += 64) {
     int t = s.efc_type[r], id = s.efc_id[r];

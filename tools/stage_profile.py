@@ -82,7 +82,7 @@ def main():
     ms = ev[0].elapsed_time(ev[1]) / a.steps
     p = _native.stage_profile(reset=True)
     sub = max(1, p["substeps"])
-    names = _native.STAGES + _native.SUBSTAGES
+    names = _native.STAGES + _native.SUBSTAGES + _native.EXTRA_STAGES
     tot = sum(p[k] for k in names)
     rows = {k: dict(cycles_per_wave_substep=round(p[k] / sub, 1), frac=round(p[k] / max(tot, 1), 4))
             for k in names}
