@@ -39,6 +39,9 @@ using namespace aw;
 #ifndef AW_KSTEP_ATTR
 #define AW_KSTEP_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
 #endif
+#ifndef AW_XCD_MAP
+#define AW_XCD_MAP 0
+#endif
 
 #ifdef AW_STAGE_PROF
 #if defined(AW_TASK_TU) || defined(AW_API_TU)
@@ -422,7 +425,19 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
   // env blockIdx.x first, then the next unclaimed env from the launch's counter, so the per-slot
   // spill / M-factor blocks (s.slot) are rewritten in the XCD's L2 instead of streaming a
   // per-env block to memory.  Every workgroup exits once the counter passes n.
+#if AW_XCD_MAP
+  // XCD-contiguous env ranges: workgroups b and b + 8 share an XCD (round-robin dispatch,
+  // MI355X_MICROARCH.md: for speed only -- correctness never depends on it), so workgroup class
+  // g = b % 8 owns envs [n g / 8, n (g + 1) / 8) and claims them from its own counter: the
+  // neighbouring envs whose rows share a 32-byte sector (obs rows, 4-byte per-env scalars) are
+  // written through ONE L2, where the partial sectors merge before they are written back
+  const bool xmap = (int)gridDim.x < n && (gridDim.x & 7) == 0;
+  const int xend = xmap ? (int)((long long)n * ((blockIdx.x & 7) + 1) / 8) : n;
+  for (int env = xmap ? (int)((long long)n * (blockIdx.x & 7) / 8) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+       env < xend;) {
+#else
   for (int env = blockIdx.x; env < n;) {
+#endif
     wsync();
     AW_PROF_START(s);
     {
@@ -517,10 +532,16 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
 #endif
     if ((int)gridDim.x >= n) break;            // one env per workgroup: no counter
     int claim = 0;
+#if AW_XCD_MAP
+    if (lane == 0) claim = atomicAdd(next_env + (blockIdx.x & 7), 1);
+    // the class's first env + its first-round share (gridDim.x / 8 workgroups) + the claim
+    env = (int)((long long)n * (blockIdx.x & 7) / 8) + (int)(gridDim.x >> 3) + __builtin_amdgcn_readfirstlane(claim);
+#else
     if (lane == 0) claim = atomicAdd(next_env, 1);
     // readfirstlane, not a shuffle: env stays a scalar, so the addresses formed from it are
     // SGPR values instead of per-lane 64-bit VGPR pairs spilled to scratch once per env
     env = (int)gridDim.x + __builtin_amdgcn_readfirstlane(claim);
+#endif
   }
 }
 
@@ -1140,7 +1161,7 @@ static void launch_step(aw_handle* h, const float* a, float* obs, float* rew, ui
                         float* tobs, int autoreset, uint64_t seed, hipStream_t st) {
   // grid = the handle's persistent slot count (aw_create / aw_set_option), capped at nenv
   const int grid = std::min(h->nenv, h->slots);
-  if (grid < h->nenv) (void)hipMemsetAsync(h->next_env, 0, sizeof(int), st);
+  if (grid < h->nenv) (void)hipMemsetAsync(h->next_env, 0, 8 * sizeof(int), st);   // one counter per XCD class
   hipLaunchKernelGGL((k_step<TASK>), dim3(grid), dim3(64), 0, st, h->m, (const DModel*)h->dmhdr, h->st, h->nenv, a, obs, rew, done,
                      goal, tobs, autoreset, seed, h->next_env);
 }
@@ -1285,7 +1306,7 @@ int aw_create(const void* blob, size_t nbytes, int n_envs, int device, aw_handle
   h->m.d = (const MData*)h->dmodel;
   HIPCHK(hipMalloc((void**)&h->m.jspill, (size_t)n_envs * JSPILL * sizeof(float)));
   HIPCHK(hipMalloc(&h->dmhdr, sizeof(DModel) + sizeof(DState)));
-  HIPCHK(hipMalloc((void**)&h->next_env, sizeof(int)));
+  HIPCHK(hipMalloc((void**)&h->next_env, 8 * sizeof(int)));
   const size_t bytes = layout_state(h.get(), nullptr);   // dry run: sizes only
   HIPCHK(hipMalloc(&h->dstate, bytes));
   HIPCHK(hipMemset(h->dstate, 0, bytes));

@@ -15,6 +15,7 @@
 namespace aw {
 
 constexpr int MAXV = 36;      // dofs (relocate: 36)
+constexpr int CHOL_P = 4;      // Cholesky panel width (aw_solver.h chol_factor)
 constexpr int VS = 36;        // J row stride: 144 B rows keep 16-byte alignment, so broadcast reads of a row are ds_read_b128
 constexpr int MAXB = 32;      // bodies incl. world
 constexpr int MAXG = 36;      // collidable geoms (compact list)
@@ -236,7 +237,7 @@ struct __attribute__((aligned(16))) Env {
       };
     };
     struct {  // phase S
-      float4 colbuf[16];      // Cholesky column broadcast (64 floats, 16-byte aligned for b128 reads)
+      float4 colbuf[MAXV];    // Cholesky panel broadcast: row k's U_k,j0..j0+3 (b128 reads)
       float L[NPACK];         // Cholesky factor, packed lower triangle (rows padded to 4)
       float vec[MAXV], vec2[MAXV], hdiag[MAXV];
     };
@@ -280,6 +281,15 @@ constexpr int KIN64_OFF = MAXPAIR * 2;
 static_assert(KIN64_OFF % 16 == 0 && KIN64_OFF + MAXB * 8 * 8 <= JL * VS * 4, "fp64 frames do not fit in the dense-J rows");
 AW_DEV double* kin64(Env& s, int b) {
   return reinterpret_cast<double*>(reinterpret_cast<char*>(&s.J[0][0]) + KIN64_OFF) + 8 * b;
+}
+#ifndef AW_KIN64_PAR
+#define AW_KIN64_PAR 0
+#endif
+// the hinge half-angle (sin, cos) of joint j, after the frames
+constexpr int KIN64_SC_OFF = KIN64_OFF + MAXB * 8 * 8;
+static_assert(KIN64_SC_OFF + MAXV * 2 * 8 <= JL * VS * 4, "fp64 joint sincos do not fit in the dense-J rows");
+AW_DEV double* kin64_sc(Env& s, int j) {
+  return reinterpret_cast<double*>(reinterpret_cast<char*>(&s.J[0][0]) + KIN64_SC_OFF) + 2 * j;
 }
 
 // ---------------------------------------------------------------------------------------

@@ -202,6 +202,19 @@ AW_DEV void stage_kin64(const DModel& m, Env& s, int lane) {
     X[0] = X[1] = X[2] = 0.0;
     X[3] = 1.0; X[4] = X[5] = X[6] = 0.0;
   }
+#if AW_KIN64_PAR
+  // the hinge half-angle sines / cosines of every needed body, one joint per lane up front: the
+  // level loop below is left with the frame algebra on its serial chain (same sincos, same
+  // inputs: bitwise the per-level evaluation)
+  const int jl = lane < m.njnt ? lane : 0;
+  if (lane < m.njnt && ((s.kin64_mask >> MD(jnt_bodyid, jl)) & 1ull) && MD(jnt_type, jl) != JNT_SLIDE) {
+    double sn, cs;
+    sincos((double)s.qpos[jl] * 0.5, &sn, &cs);
+    double* SC = kin64_sc(s, jl);
+    SC[0] = sn;
+    SC[1] = cs;
+  }
+#endif
   wsync();
   const bool own = lane > 0 && lane < m.nbody && ((s.kin64_mask >> lane) & 1ull);
   const int b = own ? lane : 0;
@@ -233,7 +246,13 @@ AW_DEV void stage_kin64(const DModel& m, Env& s, int lane) {
           rotvq(xanchor, jp, xq);
           add3(xanchor, xanchor, xp);
           double sn, cs, ql[4], v[3];
+#if AW_KIN64_PAR
+          (void)q;
+          sn = kin64_sc(s, j)[0];
+          cs = kin64_sc(s, j)[1];
+#else
           sincos(q * 0.5, &sn, &cs);
+#endif
           ql[0] = cs; ql[1] = axis[0] * sn; ql[2] = axis[1] * sn; ql[3] = axis[2] * sn;
           mulq(xq, xq, ql);
           rotvq(v, jp, xq);
