@@ -573,19 +573,6 @@ template <class T> AW_DEV bool eq(T a, T b) {
   return fb > fa ? ab < EPS_T<T> * fb : ab < EPS_T<T> * fa;
 }
 template <class T> AW_DEV bool veq(const T* a, const T* b) { return eq(a[0], b[0]) && eq(a[1], b[1]) && eq(a[2], b[2]); }
-// 1 / sqrt(x): the hardware estimate refined by Newton steps (fp64: two steps from v_rsq_f64 give
-// full double precision for normal x, where the correctly rounded sqrt + divide expansions cost
-// ~3x the instructions on the MPR's serial chain: -1.4 % k_step, r04m)
-template <class T> AW_DEV T rsqrt_fast(T x) {
-  if constexpr (sizeof(T) == 8) {
-    double r = __builtin_amdgcn_rsq(x);
-    const double hx = 0.5 * x;
-    r = r * fma(-hx * r, r, 1.5);
-    r = r * fma(-hx * r, r, 1.5);
-    return r;
-  }
-  return T(1.0) / sqrt(x);
-}
 template <class T> AW_DEV void vnorm(T* v) {
   T k = rsqrt_fast(dot3(v, v));
   scl3(v, v, k);

@@ -282,9 +282,6 @@ static_assert(KIN64_OFF % 16 == 0 && KIN64_OFF + MAXB * 8 * 8 <= JL * VS * 4, "f
 AW_DEV double* kin64(Env& s, int b) {
   return reinterpret_cast<double*>(reinterpret_cast<char*>(&s.J[0][0]) + KIN64_OFF) + 8 * b;
 }
-#ifndef AW_KIN64_PAR
-#define AW_KIN64_PAR 0
-#endif
 // the hinge half-angle (sin, cos) of joint j, after the frames
 constexpr int KIN64_SC_OFF = KIN64_OFF + MAXB * 8 * 8;
 static_assert(KIN64_SC_OFF + MAXV * 2 * 8 <= JL * VS * 4, "fp64 joint sincos do not fit in the dense-J rows");

@@ -178,6 +178,20 @@ AW_DEV void stage_kinematics(const DModel& m, Env& s, int lane) {
   wsync();
 }
 
+// 1 / sqrt(x): the hardware estimate refined by Newton steps (fp64: two steps from v_rsq_f64 give
+// full double precision for normal x, where the correctly rounded sqrt + divide expansions cost
+// ~3x the instructions on the MPR's serial chain: -1.4 % k_step, r04m)
+template <class T> AW_DEV T rsqrt_fast(T x) {
+  if constexpr (sizeof(T) == 8) {
+    double r = __builtin_amdgcn_rsq(x);
+    const double hx = 0.5 * x;
+    r = r * fma(-hx * r, r, 1.5);
+    r = r * fma(-hx * r, r, 1.5);
+    return r;
+  }
+  return T(1.0) / sqrt(x);
+}
+
 template <int N>
 AW_DEV void apply_ovr64(const DModel& m, const Env& s, int field, int obj, double (&v)[N]) {
   for (int p = 0; p < m.nparam; p++)
@@ -196,16 +210,18 @@ AW_DEV void apply_ovr64(const DModel& m, const Env& s, int field, int obj, doubl
 // axis-angle quaternions, normalised).  MPR contact points are ill-conditioned on line / face
 // contacts (a cylinder lying on a box: rotating the cylinder by 1e-7 rad moves MuJoCo's point
 // between the ends), so MPR runs on these fp64 frames, not on the fp32 ones.
+#ifndef AW_K64N
+#define AW_K64N 0
+#endif
 AW_DEV void stage_kin64(const DModel& m, Env& s, int lane) {
   if (lane == 0) {
     double* X = kin64(s, 0);
     X[0] = X[1] = X[2] = 0.0;
     X[3] = 1.0; X[4] = X[5] = X[6] = 0.0;
   }
-#if AW_KIN64_PAR
   // the hinge half-angle sines / cosines of every needed body, one joint per lane up front: the
   // level loop below is left with the frame algebra on its serial chain (same sincos, same
-  // inputs: bitwise the per-level evaluation)
+  // inputs: bitwise the per-level evaluation; r04o A/B: -0.7 % random, -1.4 % DAPG)
   const int jl = lane < m.njnt ? lane : 0;
   if (lane < m.njnt && ((s.kin64_mask >> MD(jnt_bodyid, jl)) & 1ull) && MD(jnt_type, jl) != JNT_SLIDE) {
     double sn, cs;
@@ -214,7 +230,6 @@ AW_DEV void stage_kin64(const DModel& m, Env& s, int lane) {
     SC[0] = sn;
     SC[1] = cs;
   }
-#endif
   wsync();
   const bool own = lane > 0 && lane < m.nbody && ((s.kin64_mask >> lane) & 1ull);
   const int b = own ? lane : 0;
@@ -243,26 +258,36 @@ AW_DEV void stage_kin64(const DModel& m, Env& s, int lane) {
           rotvq(xaxis, axis, xq);
           for (int c = 0; c < 3; c++) xp[c] += xaxis[c] * q;
         } else {
+          const double sn = kin64_sc(s, j)[0], cs = kin64_sc(s, j)[1];
+          const double ql[4] = {cs, axis[0] * sn, axis[1] * sn, axis[2] * sn};
+#if AW_K64N
+          // a hinge at the body origin (the free objects' rotations) leaves xpos where it is: both
+          // anchor rotations are of the zero vector (exactly zero), so they are skipped
+          if (jp[0] == 0.0 && jp[1] == 0.0 && jp[2] == 0.0) {
+            mulq(xq, xq, ql);
+            continue;
+          }
+#endif
+          double v[3];
           rotvq(xanchor, jp, xq);
           add3(xanchor, xanchor, xp);
-          double sn, cs, ql[4], v[3];
-#if AW_KIN64_PAR
-          (void)q;
-          sn = kin64_sc(s, j)[0];
-          cs = kin64_sc(s, j)[1];
-#else
-          sincos(q * 0.5, &sn, &cs);
-#endif
-          ql[0] = cs; ql[1] = axis[0] * sn; ql[2] = axis[1] * sn; ql[3] = axis[2] * sn;
           mulq(xq, xq, ql);
           rotvq(v, jp, xq);
           sub3(xp, xanchor, v);
         }
       }
-      const double n = sqrt(xq[0] * xq[0] + xq[1] * xq[1] + xq[2] * xq[2] + xq[3] * xq[3]);
       double* X = kin64(s, b);
+#if AW_K64N
+      // normalised by one refined reciprocal square root (the oracle divides by the norm: the two
+      // differ in the last fp64 bit)
+      const double n2 = xq[0] * xq[0] + xq[1] * xq[1] + xq[2] * xq[2] + xq[3] * xq[3];
+      if (n2 < 1e-30) { X[3] = 1.0; X[4] = X[5] = X[6] = 0.0; }
+      else { const double in = rsqrt_fast(n2); for (int c = 0; c < 4; c++) X[3 + c] = xq[c] * in; }
+#else
+      const double n = sqrt(xq[0] * xq[0] + xq[1] * xq[1] + xq[2] * xq[2] + xq[3] * xq[3]);
       if (n < 1e-15) { X[3] = 1.0; X[4] = X[5] = X[6] = 0.0; }
       else for (int c = 0; c < 4; c++) X[3 + c] = xq[c] / n;
+#endif
       for (int c = 0; c < 3; c++) X[c] = xp[c];
     }
     wsync();

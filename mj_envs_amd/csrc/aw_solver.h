@@ -47,8 +47,8 @@ AW_DEV void chol_factor(float (&row)[NV], int lane_in, float& invd, Env& s) {
       if (j < NV) {
         const float dj = __builtin_amdgcn_fmed3f(rlane(row[j], j), MINVAL, 3.402823466e38f);
         const float inv = __builtin_amdgcn_rcpf(dj);
-        if (lane == j) invd = inv;
         a[t] = row[j];
+        if (lane == j) invd = inv;
         u[t] = lane > j ? a[t] * inv : 0.f;
         row[j] = u[t];
 #pragma unroll

@@ -118,7 +118,66 @@ def sq(tag):
     return out
 
 
+def waitlvl(tag):
+    """k_step's s_waitcnt exposure split by instruction class (tools/gpu_waitlvl.sh): the
+    SQ_INST_LEVEL_* counters (outstanding instructions accumulated over time, unit unknown) are
+    scaled by dependent-chain kernels whose per-instruction latency s_memtime measures
+    (tools/mb/waitlvl.hip): unit = latency x INSTS / LEVEL per class."""
+    import collections
+    src = os.path.join(REPO, "gpurun_out", tag)
+
+    def agg(path, kern):
+        a = collections.defaultdict(lambda: collections.defaultdict(float))
+        for r in csv.DictReader(open(path)):
+            if kern in r["Kernel_Name"]:
+                a[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+        return {c: sum(d.values()) / len(d) for c, d in a.items()}
+
+    lat = {}
+    for ln in open(os.path.join(src, "wl_cal.log")):
+        if ln.startswith("{") and "chain" in ln:
+            d = json.loads(ln)
+            lat[d["chain"]] = d["cycles_per_inst"]
+    cal_csv = os.path.join(src, "wl_cal", "wl_counter_collection.csv")
+    unit = {}
+    for cls, kern in (("lds", "k_lds_chain"), ("smem", "k_smem_chain"), ("vmem", "k_vmem_chain")):
+        c = agg(cal_csv, kern)
+        K = cls.upper()
+        unit[cls] = dict(latency_cycles=lat[cls], insts=c[f"SQ_INSTS_{K}"], level=c[f"SQ_INST_LEVEL_{K}"],
+                         cycles_per_level_unit=lat[cls] * c[f"SQ_INSTS_{K}"] / c[f"SQ_INST_LEVEL_{K}"])
+    k = agg(os.path.join(src, "wl_kstep", "wl_counter_collection.csv"), "k_step")
+    k2 = agg(os.path.join(src, "wl_kstep2", "wl_counter_collection.csv"), "k_step")
+    waves = k["SQ_WAVES"]
+    subs = 65536 * 5 / waves
+    life = k["SQ_WAVE_CYCLES"] * 4 / waves / subs          # shader cycles per wave-substep
+    cls_out = {}
+    for cls in ("lds", "smem", "vmem"):
+        K = cls.upper()
+        oc = k[f"SQ_INST_LEVEL_{K}"] * unit[cls]["cycles_per_level_unit"] / waves / subs
+        cls_out[cls] = dict(insts_per_wave_substep=round(k[f"SQ_INSTS_{K}"] / waves / subs, 1),
+                            avg_latency_cycles=round(oc / (k[f"SQ_INSTS_{K}"] / waves / subs), 1),
+                            outstanding_cycles_per_wave_substep=round(oc),
+                            frac_of_wave_life=round(oc / life, 4))
+    out = dict(tag=tag, kernel="k_step (hammer-v0, 65 536 envs)", calibration=unit,
+               wave_life_cycles_per_wave_substep=round(life),
+               wait_any_frac=round(k2["SQ_WAIT_ANY"] / k2["SQ_WAVE_CYCLES"], 4),
+               wait_inst_any_frac=round(k2["SQ_WAIT_INST_ANY"] / k2["SQ_WAVE_CYCLES"], 4),
+               active_inst_any_frac=round(k2["SQ_ACTIVE_INST_ANY"] / k2["SQ_WAVE_CYCLES"], 4),
+               active_valu_frac=round(k2["SQ_ACTIVE_INST_VALU"] / k2["SQ_WAVE_CYCLES"], 4),
+               valu_per_wave_substep=round(k2["SQ_INSTS_VALU"] / k2["SQ_WAVES"] / (65536 * 5 / k2["SQ_WAVES"]), 1),
+               salu_per_wave_substep=round(k2["SQ_INSTS_SALU"] / k2["SQ_WAVES"] / (65536 * 5 / k2["SQ_WAVES"]), 1),
+               by_class=cls_out,
+               note="outstanding cycles overlap (several loads in flight count several times) and overlap "
+                    "the other wave's issue: they bound, not partition, the s_waitcnt time")
+    with open(os.path.join(REPO, "profiles", f"{tag}_waitlvl_kstep.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    return out
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "waitlvl":
+        print(json.dumps(waitlvl(sys.argv[2]), indent=1))
+        sys.exit(0)
     t = sys.argv[1] if len(sys.argv) > 1 else "r01"
     main(t)
     r = sq(t)
