@@ -39,9 +39,6 @@ using namespace aw;
 #ifndef AW_KSTEP_ATTR
 #define AW_KSTEP_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
 #endif
-#ifndef AW_XCD_MAP
-#define AW_XCD_MAP 0
-#endif
 
 #ifdef AW_STAGE_PROF
 #if defined(AW_TASK_TU) || defined(AW_API_TU)
@@ -400,6 +397,29 @@ AW_DEV void reset_env(const DModel& m, Env& s, const DState& st, int env, int la
   if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
 }
 
+// The next env for a persistent k_step workgroup, XCD-aware.  Workgroups b and b + 8 share an XCD
+// (round-robin dispatch, MI355X_MICROARCH.md -- for speed only, correctness never depends on it),
+// so workgroup class c = b % 8 owns envs [n c / 8, n (c + 1) / 8): its first round takes the class's
+// first gridDim.x / 8 envs, the rest are claimed from the class's own counter.  Neighbouring envs,
+// whose rows share 32-byte sectors (state and obs rows, the 1- and 4-byte per-env scalars), are then
+// written through ONE L2, where the partial sectors merge before write-back: k_step's HBM traffic
+// 1.81 -> 1.30 KB per env-step (r04p, raw counters).  A class whose range is exhausted claims from
+// the next classes, so the tail stays balanced.  Returns n when every class is exhausted.
+AW_DEV int claim_env(int* next_env, int n, int lane) {
+  const int c0 = blockIdx.x & 7, share = gridDim.x >> 3;
+  for (int t = 0; t < 8; t++) {
+    const int c = (c0 + t) & 7;
+    const int lo = (int)((long long)n * c / 8), hi = (int)((long long)n * (c + 1) / 8);
+    if (lo + share >= hi) continue;   // the class's first round covered it
+    int k = 0;
+    if (lane == 0) k = atomicAdd(next_env + c, 1);
+    // readfirstlane: env stays a scalar (SGPR addresses, no per-lane pointer spills)
+    const int e = lo + share + __builtin_amdgcn_readfirstlane(k);
+    if (e < hi) return e;
+  }
+  return n;
+}
+
 // One launch = one env-step of every env: frame_skip x (forward + Euler), task layer, and the
 // in-kernel auto-reset.  forward<NV> has exactly ONE inlined call site (the loop below drives
 // substeps, the mj_checkAcc retry and the reset forward through it), which keeps the code
@@ -422,22 +442,15 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
   __shared__ Env s;
   const int lane = threadIdx.x;
   // Persistent workgroups: the grid is one workgroup per resident slot (launch_step); each takes
-  // env blockIdx.x first, then the next unclaimed env from the launch's counter, so the per-slot
-  // spill / M-factor blocks (s.slot) are rewritten in the XCD's L2 instead of streaming a
-  // per-env block to memory.  Every workgroup exits once the counter passes n.
-#if AW_XCD_MAP
-  // XCD-contiguous env ranges: workgroups b and b + 8 share an XCD (round-robin dispatch,
-  // MI355X_MICROARCH.md: for speed only -- correctness never depends on it), so workgroup class
-  // g = b % 8 owns envs [n g / 8, n (g + 1) / 8) and claims them from its own counter: the
-  // neighbouring envs whose rows share a 32-byte sector (obs rows, 4-byte per-env scalars) are
-  // written through ONE L2, where the partial sectors merge before they are written back
+  // a first env, then the next unclaimed ones from the launch's counters, so the per-slot spill
+  // block (s.slot) is rewritten in the XCD's L2 instead of streaming a per-env block to memory.
+  // Envs go out in XCD-contiguous ranges (claim_env above); grids that are not a multiple of 8
+  // workgroups (AW_STEP_GRID) take env blockIdx.x first and then claim from one counter.  Every
+  // workgroup exits once the counters pass n.
   const bool xmap = (int)gridDim.x < n && (gridDim.x & 7) == 0;
-  const int xend = xmap ? (int)((long long)n * ((blockIdx.x & 7) + 1) / 8) : n;
-  for (int env = xmap ? (int)((long long)n * (blockIdx.x & 7) / 8) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
-       env < xend;) {
-#else
-  for (int env = blockIdx.x; env < n;) {
-#endif
+  int env = xmap ? (int)((long long)n * (blockIdx.x & 7) / 8) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  if (xmap && env >= (int)((long long)n * ((blockIdx.x & 7) + 1) / 8)) env = claim_env(next_env, n, lane);
+  while (env < n) {
     wsync();
     AW_PROF_START(s);
     {
@@ -532,16 +545,14 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
 #endif
     if ((int)gridDim.x >= n) break;            // one env per workgroup: no counter
     int claim = 0;
-#if AW_XCD_MAP
-    if (lane == 0) claim = atomicAdd(next_env + (blockIdx.x & 7), 1);
-    // the class's first env + its first-round share (gridDim.x / 8 workgroups) + the claim
-    env = (int)((long long)n * (blockIdx.x & 7) / 8) + (int)(gridDim.x >> 3) + __builtin_amdgcn_readfirstlane(claim);
-#else
+    if (xmap) {
+      env = claim_env(next_env, n, lane);
+      continue;
+    }
     if (lane == 0) claim = atomicAdd(next_env, 1);
     // readfirstlane, not a shuffle: env stays a scalar, so the addresses formed from it are
     // SGPR values instead of per-lane 64-bit VGPR pairs spilled to scratch once per env
     env = (int)gridDim.x + __builtin_amdgcn_readfirstlane(claim);
-#endif
   }
 }
 

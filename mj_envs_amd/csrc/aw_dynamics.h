@@ -210,9 +210,6 @@ AW_DEV void apply_ovr64(const DModel& m, const Env& s, int field, int obj, doubl
 // axis-angle quaternions, normalised).  MPR contact points are ill-conditioned on line / face
 // contacts (a cylinder lying on a box: rotating the cylinder by 1e-7 rad moves MuJoCo's point
 // between the ends), so MPR runs on these fp64 frames, not on the fp32 ones.
-#ifndef AW_K64N
-#define AW_K64N 0
-#endif
 AW_DEV void stage_kin64(const DModel& m, Env& s, int lane) {
   if (lane == 0) {
     double* X = kin64(s, 0);
@@ -260,14 +257,12 @@ AW_DEV void stage_kin64(const DModel& m, Env& s, int lane) {
         } else {
           const double sn = kin64_sc(s, j)[0], cs = kin64_sc(s, j)[1];
           const double ql[4] = {cs, axis[0] * sn, axis[1] * sn, axis[2] * sn};
-#if AW_K64N
           // a hinge at the body origin (the free objects' rotations) leaves xpos where it is: both
           // anchor rotations are of the zero vector (exactly zero), so they are skipped
           if (jp[0] == 0.0 && jp[1] == 0.0 && jp[2] == 0.0) {
             mulq(xq, xq, ql);
             continue;
           }
-#endif
           double v[3];
           rotvq(xanchor, jp, xq);
           add3(xanchor, xanchor, xp);
@@ -277,17 +272,11 @@ AW_DEV void stage_kin64(const DModel& m, Env& s, int lane) {
         }
       }
       double* X = kin64(s, b);
-#if AW_K64N
       // normalised by one refined reciprocal square root (the oracle divides by the norm: the two
       // differ in the last fp64 bit)
       const double n2 = xq[0] * xq[0] + xq[1] * xq[1] + xq[2] * xq[2] + xq[3] * xq[3];
       if (n2 < 1e-30) { X[3] = 1.0; X[4] = X[5] = X[6] = 0.0; }
       else { const double in = rsqrt_fast(n2); for (int c = 0; c < 4; c++) X[3 + c] = xq[c] * in; }
-#else
-      const double n = sqrt(xq[0] * xq[0] + xq[1] * xq[1] + xq[2] * xq[2] + xq[3] * xq[3]);
-      if (n < 1e-15) { X[3] = 1.0; X[4] = X[5] = X[6] = 0.0; }
-      else for (int c = 0; c < 4; c++) X[3 + c] = xq[c] / n;
-#endif
       for (int c = 0; c < 3; c++) X[c] = xp[c];
     }
     wsync();

@@ -72,13 +72,28 @@ AW_DEV void chol_factor(float (&row)[NV], int lane_in, float& invd, Env& s) {
   }
 }
 // packed rows of U into s.L (row padding included: the factor-reuse path reloads whole 4-blocks)
+#ifndef AW_CHST
+#define AW_CHST 0
+#endif
 template <int NV>
 AW_DEV void chol_store(const float (&row)[NV], int lane_in, Env& s) {
   const int lane = opaque(lane_in);
   if (lane < NV) {
+#if AW_CHST
+    // whole 4-blocks up to the lane's own (16-byte stores; the padding past NV in the last block
+    // is written as 0 -- it is inside the row's padded length and never read as a factor entry)
+#pragma unroll
+    for (int q = 0; q < (NV + 3) / 4; q++)
+      if (4 * q <= lane)
+        *reinterpret_cast<float4*>(&s.L[tri(lane) + 4 * q]) =
+            make_float4(row[4 * q], 4 * q + 1 < NV ? row[4 * q + 1 < NV ? 4 * q + 1 : 0] : 0.f,
+                        4 * q + 2 < NV ? row[4 * q + 2 < NV ? 4 * q + 2 : 0] : 0.f,
+                        4 * q + 3 < NV ? row[4 * q + 3 < NV ? 4 * q + 3 : 0] : 0.f);
+#else
 #pragma unroll
     for (int k = 0; k < NV; k++)
       if (k <= (lane | 3)) s.L[tri(lane) + k] = row[k];
+#endif
   }
 }
 // x = inv(U D U') b, b lane-distributed; U rows in registers (forward) and packed in LDS (backward)
