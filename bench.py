@@ -161,7 +161,7 @@ def config2(blob, env_id, device, n=4096, steps=100, warmup=10):
 
 
 def pmc_traffic(envs, env_id, policy, build_id):
-    """HBM bytes per k_step launch (and the summary's FETCH calibration) from the newest committed
+    """HBM bytes per k_step launch (raw, calibrated, source, calibration) from the newest committed
     rocprofv3 --pmc summary whose run matches this one exactly -- env count, task, policy and the
     kernel build id (hash of the HIP sources + flags) -- or (None, None, None): a summary of another
     workload or another kernel revision is never reported as this run's traffic."""
@@ -175,8 +175,9 @@ def pmc_traffic(envs, env_id, policy, build_id):
             continue
         if (d.get("envs"), d.get("env_id"), d.get("policy"), d.get("kernel_build_id")) == \
                 (envs, env_id, policy, build_id):
-            return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO), d.get("calibration")
-    return None, None, None
+            return (d.get("hbm_bytes_per_launch"), d.get("hbm_bytes_per_launch_calibrated"),
+                    os.path.relpath(path, REPO), d.get("calibration"))
+    return None, None, None, None
 
 
 def dry_run(args, shard):
@@ -393,7 +394,10 @@ def main():
         achieved = flops * n / (kern_ms * 1e-3) / 1e12
         bytes_step = perfmodel.step_bytes(sim.nq, sim.nv, sim.nu, sim.obs_dim, sim.nparam)
         build_id = _native.kernel_build_id()
-        traffic, pmc_src, pmc_cal = pmc_traffic(n, env_id, args.policy, build_id)
+        traffic_raw, traffic_cal, pmc_src, pmc_cal = pmc_traffic(n, env_id, args.policy, build_id)
+        # the roofline's traffic: counter bytes divided by the same box's calibration for k_step's
+        # access pattern when the summary has one, else the raw counters
+        traffic = traffic_cal or traffic_raw
         roof = dict(bound="valu", achieved=round(achieved, 3), peak=perfmodel.PEAK_FP32_TFLOPS,
                     unit="TFLOP/s", frac=round(achieved / perfmodel.PEAK_FP32_TFLOPS, 5), traffic=traffic,
                     kernel=f"k_step<{sim.task_kind}>", nv=sim.nv, kernel_ms=round(kern_ms, 4),
@@ -410,6 +414,9 @@ def main():
                     if traffic else None, pmc_source=pmc_src, pmc_calibration=pmc_cal, kernel_build_id=build_id,
                     traffic_bytes_per_env_step=round(traffic / n, 1) if traffic else None,
                     traffic_over_algorithmic=round(traffic / n / bytes_step, 3) if traffic else None,
+                    traffic_calibrated=traffic_cal is not None,
+                    traffic_raw_bytes_per_env_step=round(traffic_raw / n, 1) if traffic_raw else None,
+                    traffic_raw_over_algorithmic=round(traffic_raw / n / bytes_step, 3) if traffic_raw else None,
                     note="FP32 roofline (157.3 TFLOP/s: the vector peak, equal to the fp32 MFMA peak the contact Hessian J'DJ, "
                          "the CRB mass-matrix product and the noslip pair coupling run on); FLOPs "
                          "from perfmodel.py on profiles/work_counts_hammer.json. The HBM figures are far from "

@@ -148,6 +148,42 @@ def test_shards_bitwise_equal_to_one_batch(env_id):
     assert torch.equal(o1, o2) and torch.equal(r1, r2) and torch.equal(e1, e2) and torch.equal(t1, t2)
 
 
+@pytest.mark.parametrize("n", [2049, 6149, 16387])
+def test_persistent_claims_cover_every_env_once(n):
+    """k_step's persistent grid hands envs out in XCD-contiguous ranges with per-class counters
+    and stealing (adroit_wave.hip claim_env): with env counts that split unevenly over the eight
+    classes, every env is stepped exactly once per launch (ep_len) and the states equal, bit for
+    bit, a launch with one workgroup per env (AW_STEP_GRID=0) and one with an odd grid of 1 001
+    workgroups on the single-counter path."""
+    steps, seed = 3, 11
+    res = []
+    for grid in (None, "0", "1001"):
+        old = os.environ.pop("AW_STEP_GRID", None)
+        if grid is not None:
+            os.environ["AW_STEP_GRID"] = grid
+        try:
+            _, s = _sim("hammer-v0", n)
+        finally:
+            os.environ.pop("AW_STEP_GRID", None)
+            if old is not None:
+                os.environ["AW_STEP_GRID"] = old
+        obs, rew, done, goal = _bufs(s, n)
+        act = s.empty(n, s.nu)
+        s.reset(obs, seed=seed)
+        for k in range(steps):
+            s.random_actions(act, 9, k)
+            s.step(act, obs, rew, done, goal, autoreset=False, seed=seed)
+        ep_len = s.empty(n, dtype=torch.int32)
+        s.get_episode(ep_len=ep_len)
+        qpos = s.empty(n, s.nq)
+        s.get_state(qpos=qpos)
+        torch.cuda.synchronize()
+        assert torch.all(ep_len == steps), f"grid {grid}: env step counts {torch.unique(ep_len).tolist()}"
+        res.append((obs.clone(), qpos.clone(), rew.clone()))
+    for o, q, r in res[1:]:
+        assert torch.equal(o, res[0][0]) and torch.equal(q, res[0][1]) and torch.equal(r, res[0][2])
+
+
 def test_global_offset_changes_streams():
     """Envs at different global ids draw different resets / actions (the offset is live)."""
     _, a = _sim("relocate-v0", 64, env_offset=0)

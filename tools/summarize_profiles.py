@@ -61,6 +61,19 @@ def main(tag):
     fetch_b = statistics.mean(fetch) * 1024
     write_b = statistics.mean(write) * 1024
     nu = 26 if "hammer" in pb["config"]["workload"] else None
+    # counter calibration on the same box (tools/mb/calib.hip: one wave per 132-byte row, 4 B per
+    # lane -- k_step's state / obs pattern -- with exactly known bytes): counter / exact per direction
+    cal_pat = None
+    cf = os.path.join(src, "cal_fetch", "cf_counter_collection.csv")
+    cw = os.path.join(src, "cal_write", "cw_counter_collection.csv")
+    if os.path.exists(cf) and os.path.exists(cw):
+        ex = last_json(os.path.join(src, "cal_fetch.log"))
+        f_c, _ = pmc(cf, "FETCH_SIZE", "k_calib_read")
+        w_c, _ = pmc(cw, "WRITE_SIZE", "k_calib_write")
+        cal_pat = dict(kernels="tools/mb/calib.hip k_calib_read / k_calib_write",
+                       exact_read_bytes=ex["exact_read_bytes"], exact_write_bytes=ex["exact_write_bytes"],
+                       fetch_ratio=round(statistics.mean(f_c) * 1024 / ex["exact_read_bytes"], 4),
+                       write_ratio=round(statistics.mean(w_c) * 1024 / ex["exact_write_bytes"], 4))
     out = dict(
         tag=tag, kernel=meta["name"], envs=envs, launches=len(fetch),
         env_id=pb["config"].get("env_id"), policy=pb["config"].get("policy"),
@@ -75,15 +88,20 @@ def main(tag):
             write_size_bytes=round(statistics.mean(cal) * 1024),
             ratio=round(statistics.mean(cal) * 1024 / (envs * nu * 4), 3)),
         kernel_resources=dict((k, meta[k]) for k in ("wg", "lds", "scratch", "vgpr", "sgpr")),
+        calibration=cal_pat,
+        hbm_bytes_per_launch_calibrated=None if cal_pat is None else round(
+            fetch_b / cal_pat["fetch_ratio"] + write_b / cal_pat["write_ratio"]),
         method="rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
                "`python bench.py --steps 3 --warmup 1 --no-cpu-baseline` (MI355X_MICROARCH.md HBM section); "
                "counters are KB (x1024). FETCH_SIZE is NOT doubled: the 1/2 tally the guide documents is for "
                "16 B/lane streaming reads, while k_step reads each env's state as one 4 B/lane row per wave "
-               "(uncalibrated width); raw counter bytes are reported.")
+               "(uncalibrated width); raw counter bytes are reported, and beside them the bytes divided by "
+               "the same box's calibration for exactly that pattern (calibration).")
     with open(os.path.join(dst, f"{tag}_pmc_kstep.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps({k: out[k] for k in ("envs", "hbm_bytes_per_launch", "hbm_bytes_per_env_step",
-                                          "algorithmic_bytes_per_env_step", "write_calibration")}))
+                                          "algorithmic_bytes_per_env_step", "write_calibration",
+                                          "calibration", "hbm_bytes_per_launch_calibrated")}))
 
 
 def sq(tag):
@@ -146,7 +164,11 @@ def waitlvl(tag):
         unit[cls] = dict(latency_cycles=lat[cls], insts=c[f"SQ_INSTS_{K}"], level=c[f"SQ_INST_LEVEL_{K}"],
                          cycles_per_level_unit=lat[cls] * c[f"SQ_INSTS_{K}"] / c[f"SQ_INST_LEVEL_{K}"])
     k = agg(os.path.join(src, "wl_kstep", "wl_counter_collection.csv"), "k_step")
-    k2 = agg(os.path.join(src, "wl_kstep2", "wl_counter_collection.csv"), "k_step")
+    k2 = {}   # WAIT / ACTIVE / INSTS_VALU / SALU: tools/gpu_waitlvl.sh's second pass, or gpu_prof.sh's sq1 + sq2
+    for f in (("wl_kstep2", "wl"), ("sq1", "sq1"), ("sq2", "sq2")):
+        path = os.path.join(src, f[0], f"{f[1]}_counter_collection.csv")
+        if os.path.exists(path):
+            k2.update(agg(path, "k_step"))
     waves = k["SQ_WAVES"]
     subs = 65536 * 5 / waves
     life = k["SQ_WAVE_CYCLES"] * 4 / waves / subs          # shader cycles per wave-substep
