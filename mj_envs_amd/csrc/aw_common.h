@@ -295,16 +295,6 @@ AW_DEV float rlane(float x, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
 }
 AW_DEV int rlane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
-// (lane in MK) ? b : a for a lane mask known at compile time (unrolled loops): VCC is set by the
-// scalar unit from two immediates, so the select costs one vector instruction and no compare
-AW_DEV float sel_vcc(float a, float b, unsigned long long mk) {
-  float r;
-  asm("s_mov_b32 vcc_lo, %2\n\ts_mov_b32 vcc_hi, %3\n\tv_cndmask_b32_e32 %0, %1, %4, vcc"
-      : "=v"(r)
-      : "v"(a), "i"((int)(unsigned)(mk & 0xffffffffull)), "i"((int)(unsigned)(mk >> 32)), "v"(b)
-      : "vcc");
-  return r;
-}
 // b in lane l, a in the other lanes: v_cndmask against the constant lane mask 1 << l (an SGPR
 // constant, no v_cmp); l must be a compile-time constant after unrolling
 AW_DEV float sel_lane(float a, float b, int l) {
