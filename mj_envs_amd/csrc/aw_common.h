@@ -282,11 +282,12 @@ static_assert(KIN64_OFF % 16 == 0 && KIN64_OFF + MAXB * 8 * 8 <= JL * VS * 4, "f
 AW_DEV double* kin64(Env& s, int b) {
   return reinterpret_cast<double*>(reinterpret_cast<char*>(&s.J[0][0]) + KIN64_OFF) + 8 * b;
 }
-// the hinge half-angle (sin, cos) of joint j, after the frames
+// joint j's record for stage_kin64 (half-angle sin / cos, axis, kind), after the frames
 constexpr int KIN64_SC_OFF = KIN64_OFF + MAXB * 8 * 8;
-static_assert(KIN64_SC_OFF + MAXV * 2 * 8 <= JL * VS * 4, "fp64 joint sincos do not fit in the dense-J rows");
+constexpr int KIN64_SC_W = 6;   // doubles per joint record: sin, cos (hinges), axis, kind
+static_assert(KIN64_SC_OFF + MAXV * KIN64_SC_W * 8 <= JL * VS * 4, "fp64 joint records do not fit in the dense-J rows");
 AW_DEV double* kin64_sc(Env& s, int j) {
-  return reinterpret_cast<double*>(reinterpret_cast<char*>(&s.J[0][0]) + KIN64_SC_OFF) + 2 * j;
+  return reinterpret_cast<double*>(reinterpret_cast<char*>(&s.J[0][0]) + KIN64_SC_OFF) + KIN64_SC_W * j;
 }
 
 // ---------------------------------------------------------------------------------------

@@ -216,16 +216,25 @@ AW_DEV void stage_kin64(const DModel& m, Env& s, int lane) {
     X[0] = X[1] = X[2] = 0.0;
     X[3] = 1.0; X[4] = X[5] = X[6] = 0.0;
   }
-  // the hinge half-angle sines / cosines of every needed body, one joint per lane up front: the
-  // level loop below is left with the frame algebra on its serial chain (same sincos, same
-  // inputs: bitwise the per-level evaluation; r04o A/B: -0.7 % random, -1.4 % DAPG)
+  // one joint per lane up front, for every joint of a needed body: its record in LDS -- the hinge
+  // half-angle sin / cos, the axis and its kind (0 hinge at the body origin, 1 slide, 2 hinge with
+  // an anchor arm).  The level loop below is left with the frame algebra on its serial chain and
+  // reads LDS instead of waiting on model-table loads joint by joint (same sincos, same inputs:
+  // bitwise the per-level evaluation; r04o A/B: -0.7 % random, -1.4 % DAPG for the sincos, r04r
+  // -0.5 % random for the records)
   const int jl = lane < m.njnt ? lane : 0;
-  if (lane < m.njnt && ((s.kin64_mask >> MD(jnt_bodyid, jl)) & 1ull) && MD(jnt_type, jl) != JNT_SLIDE) {
-    double sn, cs;
-    sincos((double)s.qpos[jl] * 0.5, &sn, &cs);
+  if (lane < m.njnt && ((s.kin64_mask >> MD(jnt_bodyid, jl)) & 1ull)) {
     double* SC = kin64_sc(s, jl);
+    const bool slide = MD(jnt_type, jl) == JNT_SLIDE;
+    double sn = 0.0, cs = 1.0;
+    if (!slide) sincos((double)s.qpos[jl] * 0.5, &sn, &cs);
+    const double p0 = MD(jnt_pos64, 3 * jl), p1 = MD(jnt_pos64, 3 * jl + 1), p2 = MD(jnt_pos64, 3 * jl + 2);
     SC[0] = sn;
     SC[1] = cs;
+    SC[2] = MD(jnt_axis64, 3 * jl);
+    SC[3] = MD(jnt_axis64, 3 * jl + 1);
+    SC[4] = MD(jnt_axis64, 3 * jl + 2);
+    SC[5] = slide ? 1.0 : (p0 == 0.0 && p1 == 0.0 && p2 == 0.0 ? 0.0 : 2.0);
   }
   wsync();
   const bool own = lane > 0 && lane < m.nbody && ((s.kin64_mask >> lane) & 1ull);
@@ -248,28 +257,30 @@ AW_DEV void stage_kin64(const DModel& m, Env& s, int lane) {
       for (int k = 0; k < dn; k++) {
         const int j = da + k;
         double axis[3], jp[3], xanchor[3];
-        for (int c = 0; c < 3; c++) { axis[c] = MD(jnt_axis64, 3 * j + c); jp[c] = MD(jnt_pos64, 3 * j + c); }
-        const double q = (double)s.qpos[j];
-        if (MD(jnt_type, j) == JNT_SLIDE) {
+        const double* SCj = kin64_sc(s, j);
+        for (int c = 0; c < 3; c++) axis[c] = SCj[2 + c];
+        const double kind = SCj[5];
+        if (kind == 1.0) {
+          const double qj = (double)s.qpos[j];
           double xaxis[3];
           rotvq(xaxis, axis, xq);
-          for (int c = 0; c < 3; c++) xp[c] += xaxis[c] * q;
-        } else {
-          const double sn = kin64_sc(s, j)[0], cs = kin64_sc(s, j)[1];
-          const double ql[4] = {cs, axis[0] * sn, axis[1] * sn, axis[2] * sn};
-          // a hinge at the body origin (the free objects' rotations) leaves xpos where it is: both
-          // anchor rotations are of the zero vector (exactly zero), so they are skipped
-          if (jp[0] == 0.0 && jp[1] == 0.0 && jp[2] == 0.0) {
-            mulq(xq, xq, ql);
-            continue;
-          }
-          double v[3];
-          rotvq(xanchor, jp, xq);
-          add3(xanchor, xanchor, xp);
-          mulq(xq, xq, ql);
-          rotvq(v, jp, xq);
-          sub3(xp, xanchor, v);
+          for (int c = 0; c < 3; c++) xp[c] += xaxis[c] * qj;
+          continue;
         }
+        const double qs[4] = {SCj[1], axis[0] * SCj[0], axis[1] * SCj[0], axis[2] * SCj[0]};
+        if (kind == 0.0) {
+          mulq(xq, xq, qs);
+          continue;
+        }
+        // a hinge with an anchor arm (kind 2); a hinge at the body origin (kind 0, the free objects'
+        // rotations) skipped both anchor rotations above: they are rotations of the zero vector
+        double v[3];
+        for (int c = 0; c < 3; c++) jp[c] = MD(jnt_pos64, 3 * j + c);
+        rotvq(xanchor, jp, xq);
+        add3(xanchor, xanchor, xp);
+        mulq(xq, xq, qs);
+        rotvq(v, jp, xq);
+        sub3(xp, xanchor, v);
       }
       double* X = kin64(s, b);
       // normalised by one refined reciprocal square root (the oracle divides by the norm: the two
