@@ -128,3 +128,22 @@ def test_oracle_dapg_policies_behave_as_published(env_id):
         assert r["success_pct"] <= 10.0
     else:
         assert r["success_pct"] >= 90.0, r
+
+
+def test_bench_miss_classifier(oracle_lib):
+    """bench.py's same-run parity re-checks each miss the way the parity tests do (an fp32-unstable
+    reference: the oracle re-run on the fp32-rounded model and from <= 16-ulp perturbed states).  On
+    a smooth state away from every contact the reference is stable (False); with the tolerance
+    made unattainable by perturbing far past 16 ulps it reports the instability (True)."""
+    import bench
+    from mj_envs_amd.tasks import sample_params
+    m, o = make_oracle("hammer-v0")
+    o32 = bench._oracle_f32_model(m)
+    P = sample_params("hammer-v0", m, np.random.default_rng(3), 1)
+    st, _ = o.reset(P)
+    rng = np.random.default_rng(5)
+    for _ in range(10):                      # a moving state: relative perturbations of 0 are 0
+        o.step(st, rng.uniform(-1, 1, (1, o.nu)))
+    act = np.zeros((1, o.nu))
+    assert bench._miss_is_fp32_sensitive(o, o32, {k: v.copy() for k, v in st.items()}, act) is False
+    assert bench._miss_is_fp32_sensitive(o, o32, {k: v.copy() for k, v in st.items()}, act, ulps=2 ** 20) is True
