@@ -1,5 +1,5 @@
 // calib.hip -- FETCH_SIZE / WRITE_SIZE calibration for k_step's access pattern (run under
-// rocprofv3 --pmc FETCH_SIZE or --pmc WRITE_SIZE on the GPU box; tools/gpu_prof_r04.sh).
+// rocprofv3 --pmc FETCH_SIZE or --pmc WRITE_SIZE on the GPU box; tools/gpu_prof.sh).
 //
 // k_step moves each env's state as rows of 4-byte words, one word per lane (lane < row length):
 // load_env / store_env / write_obs.  These kernels read / write exactly that pattern with known

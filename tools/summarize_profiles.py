@@ -1,4 +1,4 @@
-"""Copy the judged parts of a gpurun_out/<tag> pass (tools/gpu_round.sh) into profiles/.
+"""Copy the judged parts of a gpurun_out/<tag> pass (tools/gpu_pass.sh + tools/gpu_prof.sh) into profiles/.
 
     python tools/summarize_profiles.py r01
 
