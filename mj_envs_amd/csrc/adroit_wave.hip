@@ -137,6 +137,12 @@ AW_DEV void narrow_class(const DModel& m, Env& s, const short* plist, int cnt, i
     short* list = const_cast<short*>(plist) + st;
     const int nsurv = midphase<C>(m, s, list, cnt, lane);
     for (int i = lane; i < nsurv; i += 64) collide_pair<C>(m, s, list[i]);
+  } else if constexpr (C == 4) {
+    // MPR: two lanes per pair (aw_collide.h swap_pair), 32 pairs per round
+    for (int i0 = 0; i0 < cnt; i0 += 32) {
+      const int i = i0 + (lane >> 1);
+      if (i < cnt) collide_pair<C>(m, s, plist[st + i], lane & 1);
+    }
   } else {
     for (int i = lane; i < cnt; i += 64) collide_pair<C>(m, s, plist[st + i]);
   }
@@ -673,12 +679,22 @@ __global__ void __launch_bounds__(64) k_task_eval(DModel m, int n, const float* 
 
 // Test hook (aw_collide_test): the narrowphase of one primitive pair per workgroup, given world
 // poses -- exact-geometry collider tests against the oracle's colliders.
-// Lanes 0..15 call it with the same pair (gl = lane): capsule-box runs on the 16-lane row as in
-// the narrowphase, every other collider on lane 0.
+// Lanes 0..15 call it with the same pair (gl = lane): capsule-box runs on the 16-lane row and MPR
+// on lanes 0 and 1 as in the narrowphase, every other collider on lane 0.
 AW_DEV void collide_gv(const DModel& m, const GV& a, const GV& b, float margin, Emit& e, int gl) {
   const int lo = a.type, hi = b.type;   // a.type <= b.type
   if (hi == GEOM_BOX && lo == GEOM_CAPSULE) {
     c_capsule_box(a, b, margin, e, gl);
+    return;
+  }
+  if (lo != GEOM_PLANE && (lo == GEOM_CYLINDER || hi == GEOM_CYLINDER)) {   // MPR on lanes 0 and 1
+    if (gl > 1) return;
+    const GV& g = gl ? b : a;
+    mpr::GVdT<double> own;
+    for (int k = 0; k < 3; k++) { own.pos[k] = g.pos[k]; own.size[k] = g.size[k]; }
+    for (int k = 0; k < 9; k++) own.mat[k] = g.mat[k];
+    own.type = g.type;
+    c_convex64(m, own, gl, (double)margin, e);
     return;
   }
   if (gl != 0) return;
@@ -687,12 +703,6 @@ AW_DEV void collide_gv(const DModel& m, const GV& a, const GV& b, float margin, 
     else if (hi == GEOM_CAPSULE) c_plane_capsule(a, b, margin, e);
     else if (hi == GEOM_CYLINDER) c_plane_cylinder(a, b, margin, e);
     else if (hi == GEOM_BOX) c_plane_box(a, b, margin, e);
-  } else if (lo == GEOM_CYLINDER || hi == GEOM_CYLINDER) {
-    mpr::GVdT<double> ad, bd;
-    for (int k = 0; k < 3; k++) { ad.pos[k] = a.pos[k]; ad.size[k] = a.size[k]; bd.pos[k] = b.pos[k]; bd.size[k] = b.size[k]; }
-    for (int k = 0; k < 9; k++) { ad.mat[k] = a.mat[k]; bd.mat[k] = b.mat[k]; }
-    ad.type = a.type; bd.type = b.type;
-    c_convex64(m, ad, bd, (double)margin, e);
   } else if (hi == GEOM_BOX && lo == GEOM_BOX) {
     c_box_box(a, b, margin, e);
   } else if (hi == GEOM_BOX) {

@@ -144,3 +144,44 @@ def test_gpu_colliders_match_exact_geometry():
     for k, out in zip(names, res):
         ref = o.collide(CAP, CASES[k][0], CASES[k][1], [R, H, 0], BOX, np.zeros(3), I3, BOXSZ, 5e-4)
         np.testing.assert_allclose(out, ref, atol=2e-6)
+
+
+CYL = 5
+MPR_CASES = {
+    # name: (type a, pos a, mat a, size a, type b, pos b, mat b, size b) with a.type <= b.type
+    "cylinder_tilted_on_box": (CYL, np.array([0.03, -0.02, 0.05 + 0.02 - 0.003]), rot_y(0.4) @ rot_z(0.3),
+                               [0.02, 0.04, 0], BOX, np.zeros(3), I3, BOXSZ),
+    "cylinder_edge_into_box": (CYL, np.array([0.19, 0.0, 0.05 + 0.015]), rot_y(1.1), [0.015, 0.03, 0],
+                               BOX, np.zeros(3), I3, BOXSZ),
+    "capsule_across_cylinder": (CAP, np.array([0.0, 0.0, 0.029]), rot_y(np.pi / 2) @ rot_z(0.2), [0.01, 0.05, 0],
+                                CYL, np.zeros(3), rot_z(0.1), [0.02, 0.04, 0]),
+    "sphere_on_cylinder_rim": (SPHERE, np.array([0.018, 0.0, 0.04 + 0.009]), I3, [0.01, 0, 0],
+                               CYL, np.zeros(3), I3, [0.02, 0.04, 0]),
+}
+
+
+@pytest.mark.gpu
+def test_gpu_mpr_pairs_match_oracle():
+    """MPR (cylinder) pairs through the GPU narrowphase hook against the oracle's fp64 MPR, on
+    poses rounded to fp32 first (the kernel's inputs), contact by contact in emission order."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mj_envs_amd import _native
+    from mj_envs_amd.tasks import attach_task, load_model
+    m = attach_task(load_model("hammer-v0"), "hammer-v0")
+    sim = _native.Sim(m.to_blob(), 1)
+    names = sorted(MPR_CASES)
+    f32 = lambda x: np.asarray(x, np.float32).astype(np.float64)
+    cases = [[f32(v) if not isinstance(v, int) else v for v in MPR_CASES[k]] for k in names]
+    types = [[c[0], c[4]] for c in cases]
+    pos = [[c[1], c[5]] for c in cases]
+    mat = [[c[2].ravel(), c[6].ravel()] for c in cases]
+    size = [[c[3], c[7]] for c in cases]
+    res = sim.collide_test(types, pos, mat, size, [5e-4] * len(names))
+    _, o = make_oracle("hammer-v0")
+    for k, c, out in zip(names, cases, res):
+        ref = o.collide(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], 5e-4)
+        assert len(ref) >= 1, k                     # every case is a penetrating contact
+        assert out.shape == ref.shape, (k, out, ref)
+        np.testing.assert_allclose(out, ref, atol=1e-5, err_msg=k)
