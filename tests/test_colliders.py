@@ -153,7 +153,7 @@ MPR_CASES = {
                                [0.02, 0.04, 0], BOX, np.zeros(3), I3, BOXSZ),
     "cylinder_edge_into_box": (CYL, np.array([0.19, 0.0, 0.05 + 0.015]), rot_y(1.1), [0.015, 0.03, 0],
                                BOX, np.zeros(3), I3, BOXSZ),
-    "capsule_across_cylinder": (CAP, np.array([0.0, 0.0, 0.029]), rot_y(np.pi / 2) @ rot_z(0.2), [0.01, 0.05, 0],
+    "capsule_end_on_cylinder": (CAP, np.array([-0.03, 0.0, 0.0603702]), rot_y(np.pi / 2 + 0.25), [0.01, 0.05, 0],
                                 CYL, np.zeros(3), rot_z(0.1), [0.02, 0.04, 0]),
     "sphere_on_cylinder_rim": (SPHERE, np.array([0.018, 0.0, 0.04 + 0.009]), I3, [0.01, 0, 0],
                                CYL, np.zeros(3), I3, [0.02, 0.04, 0]),
@@ -163,7 +163,12 @@ MPR_CASES = {
 @pytest.mark.gpu
 def test_gpu_mpr_pairs_match_oracle():
     """MPR (cylinder) pairs through the GPU narrowphase hook against the oracle's fp64 MPR, on
-    poses rounded to fp32 first (the kernel's inputs), contact by contact in emission order."""
+    poses rounded to fp32 first (the kernel's inputs), contact by contact in emission order.
+    Point contacts only: MPR's contact point on a line / face contact is ill-conditioned (a capsule
+    lying across a cylinder's face: any point of the overlap line; GPU and oracle differ by 2e-3
+    along it while depth and normal agree).  Depth to 1e-5, normal to 1e-4, the point to 5e-4 --
+    MPR stops at mpr_tolerance, and the oracle's own point moves by up to 1e-4 under a 1e-7 rad
+    rotation of these inputs."""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -184,4 +189,6 @@ def test_gpu_mpr_pairs_match_oracle():
         ref = o.collide(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], 5e-4)
         assert len(ref) >= 1, k                     # every case is a penetrating contact
         assert out.shape == ref.shape, (k, out, ref)
-        np.testing.assert_allclose(out, ref, atol=1e-5, err_msg=k)
+        np.testing.assert_allclose(out[:, 0], ref[:, 0], atol=1e-5, err_msg=k)       # depth
+        np.testing.assert_allclose(out[:, 4:7], ref[:, 4:7], atol=1e-4, err_msg=k)   # normal
+        np.testing.assert_allclose(out[:, 1:4], ref[:, 1:4], atol=5e-4, err_msg=k)   # point
