@@ -363,8 +363,8 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
   if (lane == 0) { s.nsparse = nsparse; s.ndense = nd; s.nefc = nsparse + nd; }
   wsync();
   AW_PROF(s, PR_CS_SPARSE);
-  // dense J rows: one contact at a time, lane = dof.  The per-contact model data is gathered
-  // first with lane = contact (one round of loads) and broadcast with readlane in the loop.
+  // dense J rows.  The per-contact model data is gathered first with lane = contact (one round of
+  // loads).
   unsigned long long c_m1 = 0ull, c_m2 = 0ull;
   int c_root1 = 0, c_root2 = 0;
   float c_f0 = 0.f, c_f1 = 0.f;
@@ -374,47 +374,58 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
     c_f0 = MD(cp_friction, 5 * pair); c_f1 = MD(cp_friction, 5 * pair + 1);
   }
   const int c_pair = pair, c_dim = dim, c_r0 = lane < ncon ? s.con_efc[lane] : -1;
-  for (int c = 0; c < ncon; c++) {
-    const int r0 = rlane_i(c_r0, c);
-    if (r0 < 0) break;
-    const int pr = rlane_i(c_pair, c);
-    const int cdim = rlane_i(c_dim, c);
-    if (lane < NV) {
-      int k = lane;
-      const unsigned long long m1 = ((unsigned long long)(unsigned)rlane_i((int)(c_m1 >> 32), c) << 32) |
-                                    (unsigned)rlane_i((int)c_m1, c);
-      const unsigned long long m2 = ((unsigned long long)(unsigned)rlane_i((int)(c_m2 >> 32), c) << 32) |
-                                    (unsigned)rlane_i((int)c_m2, c);
-      const int root1 = rlane_i(c_root1, c), root2 = rlane_i(c_root2, c);
-      const float* pos = s.con_pos[c];
-      float fr[9];
-      for (int q = 0; q < 3; q++) { fr[q] = s.con_nrm[c][q]; fr[3 + q] = 0.f; }
-      make_frame(fr);
-      const float* cd = s.cdof[k];
-      float jp[3] = {0, 0, 0}, jr[3] = {0, 0, 0};
-      if ((m2 >> k) & 1ull) {
-        float off3[3], t[3];
-        sub3(off3, pos, s.subcom[root2]);
-        cross3(t, cd, off3);
-        for (int q = 0; q < 3; q++) { jr[q] += cd[q]; jp[q] += cd[3 + q] + t[q]; }
-      }
-      if ((m1 >> k) & 1ull) {
-        float off3[3], t[3];
-        sub3(off3, pos, s.subcom[root1]);
-        cross3(t, cd, off3);
-        for (int q = 0; q < 3; q++) { jr[q] -= cd[q]; jp[q] -= cd[3 + q] + t[q]; }
-      }
-      float B[6];
-      for (int q = 0; q < 3; q++) { B[q] = dot3(fr + 3 * q, jp); B[3 + q] = dot3(fr + 3 * q, jr); }
-      int d = r0 - nsparse;
-      if (cdim == 1) {
-        jput(m, s, d, k, B[0]);
-      } else {
-        for (int kk = 1; kk < cdim; kk++) {
-          const float fri = kk == 1 ? rlane(c_f0, c) : (kk == 2 ? rlane(c_f1, c) : MD(cp_friction, 5 * pr + kk - 1));
-          jput(m, s, d, k, B[0] + fri * B[kk]);
-          jput(m, s, d + 1, k, B[0] - fri * B[kk]);
-          d += 2;
+  {
+    // (contact, dof) work items flattened over the wave: ceil(ncon NV / 64) passes instead of one
+    // per contact (hammer: 33 of 64 lanes busy per contact before); each lane takes its contact's
+    // data from the contact's lane by a bpermute.  Same arithmetic per entry (r04w A/B: -1.5 %
+    // DAPG, -0.3 % random)
+    const int nlead = __popcll(__ballot(lane < ncon && c_r0 >= 0));   // contacts before any overflow
+    const int total = nlead * NV;
+    for (int base = 0; base < total; base += 64) {
+      const int w = base + lane;
+      const bool act = w < total;
+      const int c = act ? w / NV : 0;
+      const int k = act ? w - c * NV : 0;
+      const int r0 = __shfl(c_r0, c, 64);
+      const int pr = __shfl(c_pair, c, 64);
+      const int cdim = __shfl(c_dim, c, 64);
+      const unsigned long long m1 = ((unsigned long long)(unsigned)__shfl((int)(c_m1 >> 32), c, 64) << 32) |
+                                    (unsigned)__shfl((int)c_m1, c, 64);
+      const unsigned long long m2 = ((unsigned long long)(unsigned)__shfl((int)(c_m2 >> 32), c, 64) << 32) |
+                                    (unsigned)__shfl((int)c_m2, c, 64);
+      const int root1 = __shfl(c_root1, c, 64), root2 = __shfl(c_root2, c, 64);
+      const float f0 = __shfl(c_f0, c, 64), f1 = __shfl(c_f1, c, 64);
+      if (act) {
+        const float* pos = s.con_pos[c];
+        float fr[9];
+        for (int q = 0; q < 3; q++) { fr[q] = s.con_nrm[c][q]; fr[3 + q] = 0.f; }
+        make_frame(fr);
+        const float* cd = s.cdof[k];
+        float jp[3] = {0, 0, 0}, jr[3] = {0, 0, 0};
+        if ((m2 >> k) & 1ull) {
+          float off3[3], t[3];
+          sub3(off3, pos, s.subcom[root2]);
+          cross3(t, cd, off3);
+          for (int q = 0; q < 3; q++) { jr[q] += cd[q]; jp[q] += cd[3 + q] + t[q]; }
+        }
+        if ((m1 >> k) & 1ull) {
+          float off3[3], t[3];
+          sub3(off3, pos, s.subcom[root1]);
+          cross3(t, cd, off3);
+          for (int q = 0; q < 3; q++) { jr[q] -= cd[q]; jp[q] -= cd[3 + q] + t[q]; }
+        }
+        float B[6];
+        for (int q = 0; q < 3; q++) { B[q] = dot3(fr + 3 * q, jp); B[3 + q] = dot3(fr + 3 * q, jr); }
+        int d = r0 - nsparse;
+        if (cdim == 1) {
+          jput(m, s, d, k, B[0]);
+        } else {
+          for (int kk = 1; kk < cdim; kk++) {
+            const float fri = kk == 1 ? f0 : (kk == 2 ? f1 : MD(cp_friction, 5 * pr + kk - 1));
+            jput(m, s, d, k, B[0] + fri * B[kk]);
+            jput(m, s, d + 1, k, B[0] - fri * B[kk]);
+            d += 2;
+          }
         }
       }
     }
