@@ -7,6 +7,10 @@ set -e -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r03}
 mkdir -p $OUT
+# the counter-calibration programs (git-ignored binaries; built here when absent)
+for p in calib waitlvl; do
+  [ -x tools/mb/$p ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o tools/mb/$p tools/mb/$p.hip
+done
 B="bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-parity --no-config2"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o kt -- python $B > $OUT/trace.log 2>&1
 echo "[prof] trace ok"
