@@ -57,7 +57,8 @@ enum {
  * contacts, constraint rows and dense (contact) rows; the reference's are nconmax 100 /
  * njmax 500 (DAPG_assets.xml:4).  A step that needs more raises AW_ST_*_OVERFLOW.
  * GRID: workgroups of one aw_step launch (one per resident slot on the device, capped at
- * n_envs); below n_envs the persistent workgroups claim the remaining envs from a counter. */
+ * n_envs); below n_envs the persistent workgroups claim the remaining envs from per-XCD
+ * counters (contiguous env ranges per XCD, stealing once a range is exhausted). */
 enum {
   AW_DIM_NQ, AW_DIM_NV, AW_DIM_NU, AW_DIM_OBS, AW_DIM_NPARAM, AW_DIM_FRAME_SKIP,
   AW_DIM_HORIZON, AW_DIM_TASK, AW_DIM_NENV, AW_DIM_NBODY, AW_DIM_NSITE, AW_DIM_NGEOM,
