@@ -114,10 +114,12 @@ def _oracle_f32_model(m):
     return Oracle(m.to_blob())
 
 
-def _miss_is_fp32_sensitive(o, o32, st, act, trials=8, ulps=16, seed=0):
+def _miss_is_fp32_sensitive(o, o32, st, act, gpu=None, trials=8, ulps=16, seed=0, factor=4.0):
     """tests/test_gpu_parity.py _fp32_sensitive: the oracle's own env-step leaves the one-step
     tolerance when re-run on the fp32-rounded model or from the state perturbed by <= 16 fp32 ulps
-    per component -- the step is on a switch / ill-conditioned at fp32 resolution"""
+    per component -- the step is on a switch / ill-conditioned at fp32 resolution -- AND (given the
+    GPU's post-step state gpu = (qpos, qvel)) the GPU's deviation from the unperturbed fp64 result
+    is within `factor` x the largest deviation of those runs (or within tolerance), in qpos and qvel"""
     import numpy as np
     rng = np.random.default_rng(seed)
     base = {k: v.copy() for k, v in st.items()}
@@ -129,13 +131,21 @@ def _miss_is_fp32_sensitive(o, o32, st, act, trials=8, ulps=16, seed=0):
         for k in ("qpos", "qvel", "warm"):
             p[k] = st[k] * (1 + eps * rng.uniform(-1, 1, st[k].shape))
         runs.append((o, p))
+    bq, bv = base["qpos"], base["qvel"]
+    tolq = lambda q: (np.abs(q - bq) <= 2e-5 + 1e-5 * np.abs(bq)).all()
+    tolv = lambda v: (np.abs(v - bv) <= 5e-3 * (1 + np.abs(bv))).all()
+    leaves, dq, dv = False, 0.0, 0.0
     for oo, p in runs:
         oo.step(p, act)
-        okq = (np.abs(p["qpos"] - base["qpos"]) <= 2e-5 + 1e-5 * np.abs(base["qpos"])).all()
-        okv = (np.abs(p["qvel"] - base["qvel"]) <= 5e-3 * (1 + np.abs(base["qvel"]))).all()
-        if not (okq and okv):
-            return True
-    return False
+        leaves |= not (tolq(p["qpos"]) and tolv(p["qvel"]))
+        dq = max(dq, float(np.abs(p["qpos"] - bq).max()))
+        dv = max(dv, float((np.abs(p["qvel"] - bv) / (1 + np.abs(bv))).max()))
+    if not leaves or gpu is None:
+        return leaves
+    gq, gv = np.asarray(gpu[0], float).reshape(bq.shape), np.asarray(gpu[1], float).reshape(bv.shape)
+    okq = tolq(gq) or float(np.abs(gq - bq).max()) <= factor * dq
+    okv = tolv(gv) or float((np.abs(gv - bv) / (1 + np.abs(bv))).max()) <= factor * dv
+    return bool(okq and okv)
 
 
 def same_run_parity(blob, sim, n=256, model=None):
@@ -170,19 +180,26 @@ def same_run_parity(blob, sim, n=256, model=None):
     okv = (np.abs(vg - st["qvel"]) <= 5e-3 * (1 + np.abs(st["qvel"]))).all(axis=1)
     ok = okq & okv
     # every miss re-checked as the parity tests do: is the fp64 reference itself unstable at fp32
-    # resolution there (tests/test_gpu_parity.py _classify_misses, criterion b)?
+    # resolution there, with the GPU inside that instability (tests/test_gpu_parity.py
+    # _classify_misses, criterion b)?  All misses are classified.
     sens = []
-    if model is not None and (~ok).any():
+    miss_idx = np.nonzero(~ok)[0]
+    if model is not None and miss_idx.size:
         o32 = _oracle_f32_model(model)
-        for k in np.nonzero(~ok)[0][:32]:
+        for k in miss_idx:
             stk = {key: st0[key][k:k + 1].copy() for key in st0}
-            sens.append(bool(_miss_is_fp32_sensitive(o, o32, stk, g(act)[k:k + 1])))
+            sens.append(bool(_miss_is_fp32_sensitive(o, o32, stk, g(act)[k:k + 1],
+                                                     gpu=(qg[k:k + 1], vg[k:k + 1]))))
+    eq = np.abs(qg - st["qpos"]).max(axis=1)
+    ev = (np.abs(vg - st["qvel"]) / (1 + np.abs(st["qvel"]))).max(axis=1)
     return dict(envs=len(idx), handle_envs=N, grid=sim.grid, sampled="evenly over the whole batch (incl. "
                 f"{int((idx >= sim.grid).sum())} envs past the {sim.grid} resident slots)",
                 frac_within_tol=round(float(ok.mean()), 4), misses=[int(i) for i in idx[~ok]],
+                misses_classified=len(sens) if model is not None else 0,
                 misses_fp32_sensitive_reference=sum(sens), misses_unexplained=len(sens) - sum(sens)
                 if model is not None else None,
-                max_abs_qpos=float(np.abs(qg - st["qpos"]).max()),
+                max_abs_qpos=float(eq.max()), max_rel_qvel=float(ev.max()),
+                p50_abs_qpos=float(np.median(eq)), p99_abs_qpos=float(np.percentile(eq, 99)),
                 median_abs_obs=float(np.median(np.abs(obs.cpu().numpy()[idx] - o_obs))),
                 max_abs_reward=float(np.abs(rew.cpu().numpy()[idx] - o_rew).max()),
                 tolerance="qpos 2e-5 + 1e-5|q|, qvel 5e-3 (1 + |v|) per env (tests/test_gpu_parity.py)")
@@ -428,11 +445,12 @@ def main():
     sim.status(sticky=sticky)
     n_over = int(((sticky & _native.ST_OVERFLOW) != 0).sum())
     n_nan = int(((sticky & (_native.ST_BADQPOS | _native.ST_BADQVEL | _native.ST_BADQACC)) != 0).sum())
-    t = torch.tensor([elapsed, kern_ms, n_over, n_nan], dtype=torch.float64, device=dev)
+    n_wide = int(((sticky & _native.ST_WIDE) != 0).sum())
+    t = torch.tensor([elapsed, kern_ms, n_over, n_nan, n_wide], dtype=torch.float64, device=dev)
     if pg:
         dist.all_reduce(t[:2], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[2:], op=dist.ReduceOp.SUM)
-    elapsed, kern_ms, n_over, n_nan = float(t[0]), float(t[1]), int(t[2]), int(t[3])
+    elapsed, kern_ms, n_over, n_nan, n_wide = float(t[0]), float(t[1]), int(t[2]), int(t[3]), int(t[4])
     finite = bool(torch.isfinite(obs).all())
 
     if rank == 0:
@@ -502,7 +520,14 @@ def main():
                                 frame_skip=sim.frame_skip, parallelism=f"env-shard x{world}", preroll=preroll,
                                 env_id=env_id, policy=args.policy),
                     roofline=roof, finite=finite, overflow_envs=n_over, bad_state_envs=n_nan,
-                    capacities=dict(maxcon=sim.maxcon, maxefc=sim.maxefc, maxdense=sim.maxdense),
+                    wide_tier_envs=n_wide,
+                    capacities=dict(maxcon=sim.maxcon, maxefc=sim.maxefc, maxdense=sim.maxdense,
+                                    fast_tier=dict(maxcon=sim.fast_maxcon, maxefc=sim.fast_maxefc,
+                                                   maxdense=sim.fast_maxdense),
+                                    wide_tier_grid=sim.wide_grid,
+                                    note="overflow_envs: envs that dropped a constraint at MuJoCo's own caps "
+                                         "(nconmax / njmax, DAPG_assets.xml:4); wide_tier_envs: envs with >= 1 "
+                                         "env-step past the fast tier's capacities, re-run in the wide tier"),
                     episodes=episodes, exchange=exchange)
         if world == 1 and not args.no_parity:
             try:

@@ -49,20 +49,26 @@ enum {
   AW_ST_BADQPOS = 1,
   AW_ST_BADQVEL = 2,
   AW_ST_BADQACC = 4,
-  AW_ST_CON_OVERFLOW = 8,
-  AW_ST_EFC_OVERFLOW = 16
+  AW_ST_CON_OVERFLOW = 8,   /* a contact past nconmax (100) was dropped, as MuJoCo drops it */
+  AW_ST_EFC_OVERFLOW = 16,  /* a constraint row past njmax (500) was dropped, as MuJoCo drops it */
+  AW_ST_WIDE = 32           /* informational: the step ran in the wide-capacity tier (below) */
 };
 
-/* aw_dims() output order.  MAXCON / MAXEFC / MAXDENSE: the kernel's per-env capacities for
- * contacts, constraint rows and dense (contact) rows; the reference's are nconmax 100 /
- * njmax 500 (DAPG_assets.xml:4).  A step that needs more raises AW_ST_*_OVERFLOW.
+/* aw_dims() output order.  MAXCON / MAXEFC / MAXDENSE: the per-env capacities for contacts,
+ * constraint rows and dense (contact) rows -- the reference model's own, nconmax 100 / njmax 500
+ * (DAPG_assets.xml:4); a step that needs more drops what MuJoCo drops and raises
+ * AW_ST_*_OVERFLOW.  Two tiers hold them: every env-step runs in the fast tier (FAST_* capacities,
+ * two waves per SIMD); one that needs more is abandoned there before anything is written and
+ * re-run in the same aw_step / aw_reset / aw_set_state call by the wide tier (MuJoCo's
+ * capacities, WIDE_GRID persistent workgroups), which marks it AW_ST_WIDE.
  * GRID: workgroups of one aw_step launch (one per resident slot on the device, capped at
  * n_envs); below n_envs the persistent workgroups claim the remaining envs from per-XCD
  * counters (contiguous env ranges per XCD, stealing once a range is exhausted). */
 enum {
   AW_DIM_NQ, AW_DIM_NV, AW_DIM_NU, AW_DIM_OBS, AW_DIM_NPARAM, AW_DIM_FRAME_SKIP,
   AW_DIM_HORIZON, AW_DIM_TASK, AW_DIM_NENV, AW_DIM_NBODY, AW_DIM_NSITE, AW_DIM_NGEOM,
-  AW_DIM_NPAIR, AW_DIM_MAXCON, AW_DIM_MAXEFC, AW_DIM_MAXDENSE, AW_DIM_GRID, AW_NDIMS
+  AW_DIM_NPAIR, AW_DIM_MAXCON, AW_DIM_MAXEFC, AW_DIM_MAXDENSE, AW_DIM_GRID,
+  AW_DIM_FAST_MAXCON, AW_DIM_FAST_MAXEFC, AW_DIM_FAST_MAXDENSE, AW_DIM_WIDE_GRID, AW_NDIMS
 };
 
 /* model table = Model.to_blob() of mj_envs_amd/mjcf.py with the task block attached
@@ -77,6 +83,12 @@ int aw_dims(const aw_handle* h, int* dims /* [AW_NDIMS] */);
  * Waits for the device (queued steps finish with the old options), then re-uploads the model
  * header that k_step reads. */
 int aw_set_option(aw_handle* h, int disableflags, int iterations, int noslip_iterations);
+
+/* Capacity tier (test / diagnostic hook): mode 0 = automatic (the fast tier, and the wide tier
+ * for a step that needs more than the fast capacities), mode 1 = every env-step, reset and
+ * set_state forward re-run by the wide tier (the fast tier's results discarded), so a test can
+ * compare the two tiers on the same inputs.  Waits for the device. */
+int aw_set_tier(aw_handle* h, int mode);
 
 /* Reset envs (mask[e] != 0, or all if mask == NULL): qpos = qpos0, qvel = 0, warmstart = 0,
  * per-env model params from `params` [N][nparam] or, if NULL, sampled on device (Philox,

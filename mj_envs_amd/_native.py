@@ -17,11 +17,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # AW_LIB selects a diagnostic build (e.g. libadroit_hip_prof.so with the stage profiler)
 LIB_PATH = os.environ.get("AW_LIB") or os.path.join(HERE, "libadroit_hip.so")
 
-AW_NDIMS = 17
-# kernel capacities (aw_common.h; also reported by aw_dims)
+AW_NDIMS = 21
+# the fast tier's capacities (aw_common.h FAST_*; the aw_forward_dump layout uses them); the
+# effective ones are the reference model's nconmax / njmax, held by the wide tier (aw_dims)
 MAXCON, MAXEFC, MAXDENSE = 48, 192, 128
-ST_BADQPOS, ST_BADQVEL, ST_BADQACC, ST_CON_OVERFLOW, ST_EFC_OVERFLOW = 1, 2, 4, 8, 16
-ST_OVERFLOW = ST_CON_OVERFLOW | ST_EFC_OVERFLOW
+NCONMAX, NJMAX = 100, 500
+ST_BADQPOS, ST_BADQVEL, ST_BADQACC, ST_CON_OVERFLOW, ST_EFC_OVERFLOW, ST_WIDE = 1, 2, 4, 8, 16, 32
+ST_OVERFLOW = ST_CON_OVERFLOW | ST_EFC_OVERFLOW   # constraints dropped at MuJoCo's own caps
 
 
 def dump_layout(maxcon=MAXCON, maxefc=MAXEFC):
@@ -37,7 +39,7 @@ def dump_layout(maxcon=MAXCON, maxefc=MAXEFC):
 
 DUMP_LAYOUT = dump_layout()
 # why the Newton solve stopped (aw_solver.h NT_EXIT_*)
-NT_EXIT = ("max_iterations", "no_descent", "fp32_noise_floor", "improvement", "gradient")
+NT_EXIT = ("max_iterations", "no_descent", "fp32_noise_floor", "improvement", "gradient", "no_constraints")
 AW_DUMP_SIZE = 1768 + 14 * MAXCON + 4 * MAXEFC
 
 _lib = None
@@ -65,6 +67,7 @@ def load():
     L.aw_step.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_uint64, _vp]
     L.aw_random_actions.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp]
     L.aw_set_env_offset.argtypes = [_vp, ctypes.c_uint64]
+    L.aw_set_tier.argtypes = [_vp, ctypes.c_int]
     L.aw_clear_status.argtypes = [_vp, _vp]
     L.aw_episode_totals.argtypes = [_vp, _vp, _vp, _vp, _vp]
     L.aw_get_episode.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp]
@@ -93,13 +96,13 @@ def load():
     for f in ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "aw_step",
               "aw_random_actions", "aw_get_state", "aw_set_state", "aw_status", "aw_episode_stats",
               "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_set_env_offset", "aw_clear_status",
-              "aw_episode_totals", "aw_get_episode", "aw_set_episode"):
+              "aw_episode_totals", "aw_get_episode", "aw_set_episode", "aw_set_tier"):
         getattr(L, f).restype = ctypes.c_int
     _lib = L
     return L
 
 
-EXPORTS = ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_reset", "aw_step",
+EXPORTS = ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_set_tier", "aw_reset", "aw_step",
            "aw_random_actions", "aw_set_env_offset", "aw_get_state", "aw_set_state", "aw_status",
            "aw_clear_status", "aw_episode_stats", "aw_episode_totals", "aw_set_episode_totals", "aw_get_episode",
            "aw_set_episode",
@@ -184,7 +187,8 @@ class Sim:
         _check(L.aw_dims(self.h, d))
         (self.nq, self.nv, self.nu, self.obs_dim, self.nparam, self.frame_skip, self.horizon,
          self.task_kind, self.n_envs, self.nbody, self.nsite, self.ngeom, self.npair,
-         self.maxcon, self.maxefc, self.maxdense, self.grid) = list(d)
+         self.maxcon, self.maxefc, self.maxdense, self.grid, self.fast_maxcon, self.fast_maxefc,
+         self.fast_maxdense, self.wide_grid) = list(d)
         self.env_offset = 0
         if env_offset:
             self.set_env_offset(env_offset)
@@ -212,6 +216,10 @@ class Sim:
 
     def set_option(self, disableflags: int = -1, iterations: int = -1, noslip_iterations: int = -1):
         _check(load().aw_set_option(self.h, disableflags, iterations, noslip_iterations))
+
+    def set_tier(self, mode: int):
+        """0: automatic (fast tier, wide tier for overflowing env-steps); 1: wide tier only (tests)"""
+        _check(load().aw_set_tier(self.h, int(mode)))
 
     def reset(self, obs, params=None, mask=None, seed: int = 1):
         _check(load().aw_reset(self.h, _ptr(mask), _ptr(params), seed, _ptr(obs), _stream()))

@@ -71,24 +71,48 @@ struct DState {
 AW_DEV void sort_contacts(Env& s, int lane) {
   int n = s.ncon;
   if (n > MAXCON) n = MAXCON;
-  const int key = lane < n ? s.con_key[lane] : 0x7fffffff;
-  int rank = 0;
-  for (int j = 0; j < n; j++) rank += rlane_i(key, j) < key ? 1 : 0;
-  float dist = 0.f, pos[3] = {0, 0, 0}, nrm[3] = {0, 0, 0};
-  int pair = 0;
-  if (lane < n) {
-    dist = s.con_dist[lane];
-    pair = s.con_pair[lane];
-    for (int k = 0; k < 3; k++) { pos[k] = s.con_pos[lane][k]; nrm[k] = s.con_nrm[lane][k]; }
+  // lane = contact, in chunks of 64 (the wide tier's 100 contacts take two)
+  int key[NCH], rank[NCH], pair[NCH];
+  float dist[NCH], pos[NCH][3], nrm[NCH][3];
+#pragma unroll
+  for (int h = 0; h < NCH; h++) {
+    const int c = lane + 64 * h;
+    key[h] = c < n ? s.con_key[c] : 0x7fffffff;
+    rank[h] = 0;
+  }
+  if constexpr (NCH == 1) {
+    for (int j = 0; j < n; j++) rank[0] += rlane_i(key[0], j) < key[0] ? 1 : 0;
+  } else {
+    for (int j = 0; j < n; j++) {
+      const int kj = s.con_key[j];
+#pragma unroll
+      for (int h = 0; h < NCH; h++) rank[h] += kj < key[h] ? 1 : 0;
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < NCH; h++) {
+    const int c = lane + 64 * h;
+    dist[h] = 0.f;
+    pair[h] = 0;
+    for (int k = 0; k < 3; k++) pos[h][k] = nrm[h][k] = 0.f;
+    if (c < n) {
+      dist[h] = s.con_dist[c];
+      pair[h] = s.con_pair[c];
+      for (int k = 0; k < 3; k++) { pos[h][k] = s.con_pos[c][k]; nrm[h][k] = s.con_nrm[c][k]; }
+    }
   }
   wsync();
-  if (lane < n) {
-    s.con_key[rank] = key;
-    s.con_dist[rank] = dist;
-    s.con_pair[rank] = pair;
-    copy3(s.con_pos[rank], pos);
-    normalize3(nrm);              // mju_makeFrame's first step; tangents are rebuilt where used
-    copy3(s.con_nrm[rank], nrm);
+#pragma unroll
+  for (int h = 0; h < NCH; h++) {
+    if (lane + 64 * h < n) {
+      const int r = rank[h];
+      s.con_key[r] = key[h];
+      s.con_dist[r] = dist[h];
+      s.con_pair[r] = pair[h];
+      copy3(s.con_pos[r], pos[h]);
+      normalize3(nrm[h]);         // mju_makeFrame's first step; tangents are rebuilt where used
+      copy3(s.con_nrm[r], nrm[h]);
+    }
   }
   if (lane == 0) s.ncon = n;
   wsync();
@@ -245,7 +269,7 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[Tree<TASK>:
   AW_PROF(s, PR_RNE);
   stage_crb<NV>(m, s, lane, Mrow);
   AW_PROF(s, PR_CRB);
-  if (lane == 0) { s.it_newton = 0; s.it_noslip = 0; }
+  if (lane == 0) { s.it_newton = 1000 * NT_EXIT_NOROWS; s.it_noslip = 0; }
   stage_constraints<NV>(m, s, lane);
   AW_PROF(s, PR_CONSTR);
   // qacc_smooth = M \ qfrc_smooth: mj_factorM + mj_solveM over the dof tree (aw_tree.h)
@@ -403,6 +427,159 @@ AW_DEV void reset_env(const DModel& m, Env& s, const DState& st, int env, int la
   if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
 }
 
+// ---------------------------------------------------------------------------------------
+// The wide-tier queue (aw_common.h, two capacity tiers): q[0] = entries, q[1] = the wide kernel's
+// claim counter, q[2 + k] = env | kind << 30.  DK_STEP: the whole env-step is re-run from the
+// unchanged pre-step state (the fast tier wrote nothing for it); DK_FORWARD: the state, params and
+// bookkeeping are written, only mj_forward + obs are re-run (a reset / set_state forward, ctrl 0).
+enum { DK_STEP = 0, DK_FORWARD = 1 };
+constexpr unsigned ST_OVF = ST_CON_OVERFLOW | ST_EFC_OVERFLOW;
+AW_DEV void defer_env(int* q, int env, int kind, int lane) {
+  if (lane == 0) {
+    const int k = atomicAdd(q, 1);
+    q[2 + k] = env | (kind << 30);
+  }
+}
+// fast tier: did the forward just run drop a contact or a row (uniform LDS read)?  (aw_set_tier's
+// test mode sends every forward to the wide tier)
+AW_DEV bool fast_overflow(const DModel& m, const Env& s) { return !WIDE && ((s.status & ST_OVF) != 0u || m.force_wide); }
+
+// One env-step of env `env`: frame_skip x (forward + Euler), task layer, and the auto-reset.
+// forward<NV> has exactly ONE inlined call site (the loop below drives substeps, the mj_checkAcc
+// retry and the reset forward through it), which keeps the code object small enough for the
+// instruction cache.  Fast tier (defer != nullptr): a forward that overflows the fast capacities
+// abandons the env-step before anything is written and queues it for the wide tier (or, in the
+// reset forward, queues that forward alone).
+template <int TASK>
+AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lane,
+                     const float* __restrict__ actions, float* obs, float* reward, uint8_t* done, uint8_t* goal,
+                     float* terminal_obs, int autoreset, uint64_t seed, int* defer) {
+  constexpr int NV = Tree<TASK>::NV;
+  wsync();
+  AW_PROF_START(s);
+  {
+    // an opaque lane id here and in the env-step tail below: per-lane state / obs addresses
+    // are formed where they are used instead of once per env and spilled to scratch
+    const int el = AW_ENV_LANE(lane);
+    load_env<NV>(m, s, st, env, el);
+    if (WIDE && el == 0) s.status = ST_WIDE;
+    if (el < m.nu) {
+      float a = clampf(actions[(size_t)env * m.nu + el], -1.f, 1.f);
+      s.ctrl[el] = MD(act_mid, el) + a * MD(act_rng, el);
+    }
+    stage_model(m, s, st.params + (size_t)env * m.nparam, el);
+  }
+  float Mrow[NV];
+  Dof d;
+  float* ob = obs + (size_t)env * m.obs_dim;
+  int sub = 0;
+  bool resetting = false, retry = false;
+  AW_PROF(s, PR_PRE);
+#pragma nounroll
+  while (true) {
+    // memory clobber: keeps LICM from hoisting the (loop-invariant) model loads of a whole
+    // substep out of this loop, which would pin them in registers across every stage
+    asm volatile("" ::: "memory");
+    // and no lane-dependent value is hoisted out of the loop either (the lane id is re-derived
+    // per substep): loop-invariant masks and offsets would otherwise occupy SGPRs / VGPRs across
+    // every stage of the substep
+    const int sl = opaque(lane);
+    if (!resetting && !retry) check_state<NV>(s, sl);
+    AW_PROF(s, PR_CHECK);
+    forward<TASK>(m, s, sl, Mrow, d);
+    if (fast_overflow(m, s)) {
+      if (!resetting) {            // nothing of this env-step is written: the wide tier re-runs it
+        defer_env(defer, env, DK_STEP, sl);
+        return;
+      }
+      break;                       // the reset forward alone goes to the wide tier (below)
+    }
+    if (resetting) break;
+    if (!retry && check_acc<NV>(s, sl, d)) { retry = true; continue; }
+    retry = false;
+    euler<TASK>(m, s, sl, Mrow, d);
+    AW_PROF(s, PR_EULER);
+    AW_PROF_COUNT(s, PR_SUBSTEPS);
+    if (++sub < m.frame_skip) continue;
+    // env-step complete: observation, reward, episode bookkeeping
+    const int tl = AW_ENV_LANE(lane);
+    write_obs(m, s, tl, ob);
+    int term = 0, trunc = 0;
+    if (tl == 0) {
+      float r;
+      int dn, gl;
+      task_reward(m, s, &r, &dn, &gl);
+      reward[env] = r;
+      goal[env] = (uint8_t)gl;
+      int t = st.ep_len[env] + 1;
+      term = dn;
+      trunc = (m.horizon > 0 && t >= m.horizon) ? 1 : 0;
+      done[env] = (uint8_t)(term | (trunc << 1));
+      float ret = st.ep_ret[env] + r;
+      int gcount = st.ep_goal[env] + gl;
+      st.ep_len[env] = t;
+      st.ep_ret[env] = ret;
+      st.ep_goal[env] = gcount;
+      st.status[env] = s.status;
+      st.status_acc[env] |= s.status;
+      if (term || trunc) {
+        st.last_ret[env] = ret;
+        st.last_goal[env] = gcount;
+        st.last_len[env] = t;
+        st.episode[env] += 1;
+        st.sum_ret[env] += ret;
+        st.n_success[env] += gcount > m.success_steps ? 1 : 0;
+      }
+    }
+    store_env<NV>(m, s, st, env, tl);
+    AW_PROF(s, PR_TASK);
+    const int ended = __builtin_amdgcn_readfirstlane(term | trunc);
+    if (!(autoreset && ended)) break;
+    __threadfence_block();
+    if (terminal_obs)
+      for (int o = tl; o < m.obs_dim; o += 64) terminal_obs[(size_t)env * m.obs_dim + o] = s.rowbuf[o];
+    wsync();
+    reset_prepare<NV>(m, s, st, env, tl, nullptr, seed);
+    if (WIDE && tl == 0) s.status |= ST_WIDE;
+    AW_PROF(s, PR_RESET);
+    resetting = true;
+  }
+  if (resetting) {
+    const int rl = AW_ENV_LANE(lane);
+    store_env<NV>(m, s, st, env, rl);
+    if (fast_overflow(m, s)) {
+      if (rl == 0) st.status_acc[env] |= s.status & ~ST_OVF;
+      defer_env(defer, env, DK_FORWARD, rl);
+    } else {
+      write_obs(m, s, rl, ob);
+      if (rl == 0) st.status_acc[env] |= s.status;
+    }
+  }
+#ifdef AW_STAGE_PROF
+  AW_PROF(s, PR_TASK);
+  AW_PROF_COUNT(s, PR_CALLS);
+  if (lane == 0)
+    for (int i = 0; i < AW_NPROF; i++) atomicAdd(&g_stage_prof[i], s.prof_acc[i]);
+#endif
+}
+
+// mj_forward + obs of a stored state (wide tier, DK_FORWARD): ctrl 0, as after a reset / set_state
+template <int TASK>
+AW_DEV void forward_stored(const DModel& m, Env& s, const DState& st, int env, int lane, float* obs) {
+  constexpr int NV = Tree<TASK>::NV;
+  wsync();
+  load_env<NV>(m, s, st, env, lane);
+  if (lane == 0) s.status = ST_WIDE;
+  if (lane < m.nu) s.ctrl[lane] = 0.f;
+  stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
+  float Mrow[NV];
+  Dof d;
+  forward<TASK>(m, s, lane, Mrow, d);
+  if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
+  if (lane == 0) { st.status[env] |= s.status; st.status_acc[env] |= s.status; }
+}
+
+#ifndef AW_WIDE
 // The next env for a persistent k_step workgroup, XCD-aware.  Workgroups b and b + 8 share an XCD
 // (round-robin dispatch, MI355X_MICROARCH.md -- for speed only, correctness never depends on it),
 // so workgroup class c = b % 8 owns envs [n c / 8, n (c + 1) / 8): its first round takes the class's
@@ -426,17 +603,14 @@ AW_DEV int claim_env(int* next_env, int n, int lane) {
   return n;
 }
 
-// One launch = one env-step of every env: frame_skip x (forward + Euler), task layer, and the
-// in-kernel auto-reset.  forward<NV> has exactly ONE inlined call site (the loop below drives
-// substeps, the mj_checkAcc retry and the reset forward through it), which keeps the code
-// object small enough for the instruction cache.
+// One launch = one env-step of every env (fast tier).  next_env[0..7]: the per-XCD claim
+// counters, next_env[8..]: the wide-tier queue (defer_env).
 template <int TASK>
 __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DModel* __restrict__ mptr, DState stval,
                                              int n, const float* __restrict__ actions,
                                              float* obs, float* reward, uint8_t* done, uint8_t* goal,
                                              float* terminal_obs, int autoreset, uint64_t seed,
                                              int* __restrict__ next_env) {
-  constexpr int NV = Tree<TASK>::NV;
   // model scalars read from the device copy on demand (scalar loads behind the loop's memory
   // clobber) instead of ~50 kernel-argument SGPRs held live across the whole launch
   const DModel& m = *mptr;
@@ -457,98 +631,8 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
   int env = xmap ? (int)((long long)n * (blockIdx.x & 7) / 8) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   if (xmap && env >= (int)((long long)n * ((blockIdx.x & 7) + 1) / 8)) env = claim_env(next_env, n, lane);
   while (env < n) {
-    wsync();
-    AW_PROF_START(s);
-    {
-      // an opaque lane id here and in the env-step tail below: per-lane state / obs addresses
-      // are formed where they are used instead of once per env and spilled to scratch
-      const int el = AW_ENV_LANE(lane);
-      load_env<NV>(m, s, st, env, el);
-      if (el < m.nu) {
-        float a = clampf(actions[(size_t)env * m.nu + el], -1.f, 1.f);
-        s.ctrl[el] = MD(act_mid, el) + a * MD(act_rng, el);
-      }
-      stage_model(m, s, st.params + (size_t)env * m.nparam, el);
-    }
-    float Mrow[NV];
-    Dof d;
-    float* ob = obs + (size_t)env * m.obs_dim;
-    int sub = 0;
-    bool resetting = false, retry = false;
-    AW_PROF(s, PR_PRE);
-#pragma nounroll
-    while (true) {
-      // memory clobber: keeps LICM from hoisting the (loop-invariant) model loads of a whole
-      // substep out of this loop, which would pin them in registers across every stage
-      asm volatile("" ::: "memory");
-      // and no lane-dependent value is hoisted out of the loop either (the lane id is re-derived
-      // per substep): loop-invariant masks and offsets would otherwise occupy SGPRs / VGPRs across
-      // every stage of the substep
-      const int sl = opaque(lane);
-      if (!resetting && !retry) check_state<NV>(s, sl);
-      AW_PROF(s, PR_CHECK);
-      forward<TASK>(m, s, sl, Mrow, d);
-      if (resetting) break;
-      if (!retry && check_acc<NV>(s, sl, d)) { retry = true; continue; }
-      retry = false;
-      euler<TASK>(m, s, sl, Mrow, d);
-      AW_PROF(s, PR_EULER);
-      AW_PROF_COUNT(s, PR_SUBSTEPS);
-      if (++sub < m.frame_skip) continue;
-      // env-step complete: observation, reward, episode bookkeeping
-      const int tl = AW_ENV_LANE(lane);
-      write_obs(m, s, tl, ob);
-      int term = 0, trunc = 0;
-      if (tl == 0) {
-        float r;
-        int dn, gl;
-        task_reward(m, s, &r, &dn, &gl);
-        reward[env] = r;
-        goal[env] = (uint8_t)gl;
-        int t = st.ep_len[env] + 1;
-        term = dn;
-        trunc = (m.horizon > 0 && t >= m.horizon) ? 1 : 0;
-        done[env] = (uint8_t)(term | (trunc << 1));
-        float ret = st.ep_ret[env] + r;
-        int gcount = st.ep_goal[env] + gl;
-        st.ep_len[env] = t;
-        st.ep_ret[env] = ret;
-        st.ep_goal[env] = gcount;
-        st.status[env] = s.status;
-        st.status_acc[env] |= s.status;
-        if (term || trunc) {
-          st.last_ret[env] = ret;
-          st.last_goal[env] = gcount;
-          st.last_len[env] = t;
-          st.episode[env] += 1;
-          st.sum_ret[env] += ret;
-          st.n_success[env] += gcount > m.success_steps ? 1 : 0;
-        }
-      }
-      store_env<NV>(m, s, st, env, tl);
-      AW_PROF(s, PR_TASK);
-      const int ended = __builtin_amdgcn_readfirstlane(term | trunc);
-      if (!(autoreset && ended)) break;
-      __threadfence_block();
-      if (terminal_obs)
-        for (int o = tl; o < m.obs_dim; o += 64) terminal_obs[(size_t)env * m.obs_dim + o] = s.rowbuf[o];
-      wsync();
-      reset_prepare<NV>(m, s, st, env, tl, nullptr, seed);
-      AW_PROF(s, PR_RESET);
-      resetting = true;
-    }
-    if (resetting) {
-      const int rl = AW_ENV_LANE(lane);
-      write_obs(m, s, rl, ob);
-      store_env<NV>(m, s, st, env, rl);
-      if (rl == 0) st.status_acc[env] |= s.status;
-    }
-#ifdef AW_STAGE_PROF
-    AW_PROF(s, PR_TASK);
-    AW_PROF_COUNT(s, PR_CALLS);
-    if (lane == 0)
-      for (int i = 0; i < AW_NPROF; i++) atomicAdd(&g_stage_prof[i], s.prof_acc[i]);
-#endif
+    env_step<TASK>(m, s, st, env, lane, actions, obs, reward, done, goal, terminal_obs, autoreset, seed,
+                   next_env + 8);
     if ((int)gridDim.x >= n) break;            // one env per workgroup: no counter
     int claim = 0;
     if (xmap) {
@@ -564,22 +648,31 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
 
 template <int TASK>
 __global__ void __launch_bounds__(64) k_reset(DModel m, DState st, int n, const uint8_t* mask,
-                                              const float* params, uint64_t seed, float* obs) {
+                                              const float* params, uint64_t seed, float* obs, int* defer) {
   constexpr int NV = Tree<TASK>::NV;
   __shared__ Env s;
   const int env = blockIdx.x, lane = threadIdx.x;
   if (env >= n) return;
   if (mask && !mask[env]) return;
   if (lane == 0) { s.status = 0u; s.slot = blockIdx.x; }
-  reset_env<TASK>(m, s, st, env, lane, params, seed, obs);
+  reset_prepare<NV>(m, s, st, env, lane, params, seed);
+  float Mrow[NV];
+  Dof d;
+  forward<TASK>(m, s, lane, Mrow, d);
   store_env<NV>(m, s, st, env, lane);
+  if (fast_overflow(m, s)) {
+    if (lane == 0) { st.status[env] = s.status & ~ST_OVF; st.status_acc[env] |= s.status & ~ST_OVF; }
+    defer_env(defer, env, DK_FORWARD, lane);
+    return;
+  }
+  if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
   if (lane == 0) { st.status[env] = s.status; st.status_acc[env] |= s.status; }
 }
 
 template <int TASK>
 __global__ void __launch_bounds__(64) k_set_state(DModel m, DState st, int n, const float* qpos,
                                                   const float* qvel, const float* warm,
-                                                  const float* params, float* obs) {
+                                                  const float* params, float* obs, int* defer) {
   constexpr int NV = Tree<TASK>::NV;
   __shared__ Env s;
   const int env = blockIdx.x, lane = threadIdx.x;
@@ -598,11 +691,44 @@ __global__ void __launch_bounds__(64) k_set_state(DModel m, DState st, int n, co
   float Mrow[NV];
   Dof d;
   forward<TASK>(m, s, lane, Mrow, d);
-  if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
   store_env<NV>(m, s, st, env, lane);
+  if (fast_overflow(m, s)) {
+    if (lane == 0) { st.status[env] = s.status & ~ST_OVF; st.status_acc[env] |= s.status & ~ST_OVF; }
+    defer_env(defer, env, DK_FORWARD, lane);
+    return;
+  }
+  if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
   if (lane == 0) { st.status[env] = s.status; st.status_acc[env] |= s.status; }
 }
+#else  // AW_WIDE
+// The wide tier: persistent workgroups drain the queue the fast launch before it filled (q[0]
+// entries; an empty queue ends every workgroup at its first claim).  Same env-step code with
+// MuJoCo's capacities; mptr is the wide header (its jspill: one JSPILL_WIDE block per workgroup).
+template <int TASK>
+__global__ void __launch_bounds__(64) k_step_wide(const DModel* __restrict__ mptr, const float* __restrict__ actions,
+                                                  float* obs, float* reward, uint8_t* done, uint8_t* goal,
+                                                  float* terminal_obs, int autoreset, uint64_t seed,
+                                                  int* __restrict__ q) {
+  const DModel& m = *mptr;
+  const DState& st = *reinterpret_cast<const DState*>(mptr + 1);
+  __shared__ Env s;
+  const int lane = threadIdx.x;
+  while (true) {
+    int k = 0;
+    if (lane == 0) k = atomicAdd(q + 1, 1);
+    k = __builtin_amdgcn_readfirstlane(k);
+    if (k >= q[0]) break;
+    const int ent = q[2 + k];
+    const int env = ent & 0x3fffffff, kind = ent >> 30;
+    if (kind == DK_STEP)
+      env_step<TASK>(m, s, st, env, lane, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, nullptr);
+    else
+      forward_stored<TASK>(m, s, st, env, lane, obs);
+  }
+}
+#endif  // AW_WIDE
 
+#ifndef AW_WIDE   // introspection: fast tier only
 // dump layout (floats): see mj_envs_amd/_native.py dump_layout (same offsets from the capacities)
 constexpr int DUMP_SCAL = 1760, DUMP_CON = 1768, DUMP_EFC = DUMP_CON + 14 * MAXCON;
 static_assert(DUMP_EFC + 4 * MAXEFC == AW_DUMP_SIZE, "AW_DUMP_SIZE out of date");
@@ -652,6 +778,8 @@ __global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const
     out[DUMP_EFC + 3 * MAXEFC + r] = v ? (float)s.efc_type[r] : -1.f;
   }
 }
+
+#endif  // !AW_WIDE
 
 #ifndef AW_TASK_TU   // task-independent kernels: in the API translation unit only
 __global__ void __launch_bounds__(64) k_task_eval(DModel m, int n, const float* qpos, const float* qvel,
@@ -841,16 +969,24 @@ struct aw_handle {
   void* dmodel = nullptr;
   void* dmhdr = nullptr;   // device copy of m (k_step reads its scalars from here)
   void* dstate = nullptr;
-  int* next_env = nullptr;   // k_step's work counter (env claims past the first grid's worth)
+  int* next_env = nullptr;   // [0, 8): k_step's per-XCD claim counters; [8, 10 + nenv): the wide-tier
+                             // queue (count, claim counter, entries; adroit_wave.hip defer_env)
   int slots = 0;             // persistent k_step grid: resident workgroups of the selected instantiation,
                              // or AW_STEP_GRID (read at aw_create; 0 = one workgroup per env)
   int grid_env = -1;         // AW_STEP_GRID at create (-1: unset)
+  void* dmhdr_wide = nullptr;   // the wide tier's header: m with jspill -> jspill_wide, then st
+  float* jspill_wide = nullptr; // one JSPILL_WIDE block per wide workgroup
+  int wide_grid = 0;            // persistent k_step_wide workgroups (resident slots, capped at nenv)
 };
 
 #ifndef AW_TASK_TU
 static int upload_header(aw_handle* h) {
   HIPCHK(hipMemcpy(h->dmhdr, &h->m, sizeof(DModel), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy((DModel*)h->dmhdr + 1, &h->st, sizeof(DState), hipMemcpyHostToDevice));
+  DModel mw = h->m;
+  mw.jspill = h->jspill_wide;
+  HIPCHK(hipMemcpy(h->dmhdr_wide, &mw, sizeof(DModel), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy((DModel*)h->dmhdr_wide + 1, &h->st, sizeof(DState), hipMemcpyHostToDevice));
   return AW_OK;
 }
 
@@ -1169,6 +1305,34 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
 
 #endif  // AW_TASK_TU
 
+// The wide tier's launcher table, defined in the -DAW_WIDE -DAW_TASK_TU=TASK translation unit
+// (k_step_wide<TASK>): `run` drains the queue that the fast launch before it filled.
+struct WideOps {
+  int (*slots)(int device);
+  void (*run)(aw_handle*, const float*, float*, float*, uint8_t*, uint8_t*, float*, int, uint64_t, hipStream_t);
+};
+template <int TASK> const WideOps* wide_ops();
+
+#ifdef AW_WIDE
+template <int TASK>
+static int wide_slots(int device) {
+  int per_cu = 0, cus = 0;
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_step_wide<TASK>, 64, 0);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  return std::max(per_cu, 1) * std::max(cus, 1);
+}
+template <int TASK>
+static void launch_wide(aw_handle* h, const float* a, float* obs, float* rew, uint8_t* done, uint8_t* goal,
+                        float* tobs, int autoreset, uint64_t seed, hipStream_t st) {
+  hipLaunchKernelGGL((k_step_wide<TASK>), dim3(h->wide_grid), dim3(64), 0, st, (const DModel*)h->dmhdr_wide, a, obs, rew,
+                     done, goal, tobs, autoreset, seed, h->next_env + 8);
+}
+template <int TASK> const WideOps* wide_ops() {
+  static const WideOps ops = {wide_slots<TASK>, launch_wide<TASK>};
+  return &ops;
+}
+template const WideOps* wide_ops<AW_TASK_TU>();
+#else
 // resident k_step workgroups on the handle's device (occupancy x CUs): the persistent grid
 template <int TASK>
 static int step_slots(int device) {
@@ -1177,24 +1341,36 @@ static int step_slots(int device) {
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
   return std::max(per_cu, 1) * std::max(cus, 1);
 }
+// every launch that runs a fast-tier forward clears the wide queue first and drains it after
+static void clear_queue(aw_handle* h, bool counters, hipStream_t st) {
+  if (counters) (void)hipMemsetAsync(h->next_env, 0, 10 * sizeof(int), st);   // XCD counters + queue heads
+  else (void)hipMemsetAsync(h->next_env + 8, 0, 2 * sizeof(int), st);
+}
 template <int TASK>
 static void launch_step(aw_handle* h, const float* a, float* obs, float* rew, uint8_t* done, uint8_t* goal,
                         float* tobs, int autoreset, uint64_t seed, hipStream_t st) {
   // grid = the handle's persistent slot count (aw_create / aw_set_option), capped at nenv
   const int grid = std::min(h->nenv, h->slots);
-  if (grid < h->nenv) (void)hipMemsetAsync(h->next_env, 0, 8 * sizeof(int), st);   // one counter per XCD class
+  clear_queue(h, grid < h->nenv, st);
   hipLaunchKernelGGL((k_step<TASK>), dim3(grid), dim3(64), 0, st, h->m, (const DModel*)h->dmhdr, h->st, h->nenv, a, obs, rew, done,
                      goal, tobs, autoreset, seed, h->next_env);
+  wide_ops<TASK>()->run(h, a, obs, rew, done, goal, tobs, autoreset, seed, st);
 }
 template <int TASK>
 static void launch_reset(aw_handle* h, const uint8_t* mask, const float* params, uint64_t seed, float* obs,
                          hipStream_t st) {
-  hipLaunchKernelGGL((k_reset<TASK>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, mask, params, seed, obs);
+  clear_queue(h, false, st);
+  hipLaunchKernelGGL((k_reset<TASK>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, mask, params, seed, obs,
+                     h->next_env + 8);
+  wide_ops<TASK>()->run(h, nullptr, obs, nullptr, nullptr, nullptr, nullptr, 0, seed, st);
 }
 template <int TASK>
 static void launch_set(aw_handle* h, const float* q, const float* v, const float* w, const float* p, float* obs,
                        hipStream_t st) {
-  hipLaunchKernelGGL((k_set_state<TASK>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, q, v, w, p, obs);
+  clear_queue(h, false, st);
+  hipLaunchKernelGGL((k_set_state<TASK>), dim3(h->nenv), dim3(64), 0, st, h->m, h->st, h->nenv, q, v, w, p, obs,
+                     h->next_env + 8);
+  wide_ops<TASK>()->run(h, nullptr, obs, nullptr, nullptr, nullptr, nullptr, 0, 0, st);
 }
 template <int TASK>
 static void launch_dump(aw_handle* h, int env, const float* ctrl, float* out, hipStream_t st) {
@@ -1205,10 +1381,12 @@ template <int TASK>
 static void launch_depth(aw_handle* h, const CamRec& cam, int W, int H, float* out, hipStream_t st) {
   hipLaunchKernelGGL((k_depth<TASK>), dim3(h->nenv), dim3(256), 0, st, h->m, h->st, h->nenv, cam, W, H, out);
 }
+#endif  // AW_WIDE
 
 // The launchers of one task, behind one table.  Split build: task_ops<TASK> is defined (and with
 // it every kernel of TASK instantiated) only in the -DAW_TASK_TU=TASK translation unit; the API
-// unit sees the declaration and calls it across the link.
+// unit sees the declaration and calls it across the link.  The wide tier's table (wide_ops) comes
+// from the -DAW_WIDE unit of the same task in every build.
 struct TaskOps {
   int (*slots)(int device);
   void (*step)(aw_handle*, const float*, float*, float*, uint8_t*, uint8_t*, float*, int, uint64_t, hipStream_t);
@@ -1218,16 +1396,17 @@ struct TaskOps {
   void (*depth)(aw_handle*, const CamRec&, int, int, float*, hipStream_t);
 };
 template <int TASK> const TaskOps* task_ops();
-#ifndef AW_API_TU
+#if !defined(AW_API_TU) && !defined(AW_WIDE)
 template <int TASK> const TaskOps* task_ops() {
   static const TaskOps ops = {step_slots<TASK>, launch_step<TASK>, launch_reset<TASK>, launch_set<TASK>,
                               launch_dump<TASK>, launch_depth<TASK>};
   return &ops;
 }
 #endif
-#ifdef AW_TASK_TU
+#if defined(AW_TASK_TU) && !defined(AW_WIDE)
 template const TaskOps* task_ops<AW_TASK_TU>();
-#else
+#endif
+#ifndef AW_TASK_TU
 
 // kernels are instantiated per task (the dof tree of aw_trees.h is a template argument)
 #ifdef AW_ONLY_TASK
@@ -1293,6 +1472,8 @@ static void free_handle(aw_handle* h) {
   if (h->dstate) (void)hipFree(h->dstate);
   if (h->m.jspill) (void)hipFree(h->m.jspill);
   if (h->next_env) (void)hipFree(h->next_env);
+  if (h->dmhdr_wide) (void)hipFree(h->dmhdr_wide);
+  if (h->jspill_wide) (void)hipFree(h->jspill_wide);
   delete h;
 }
 
@@ -1325,9 +1506,17 @@ int aw_create(const void* blob, size_t nbytes, int n_envs, int device, aw_handle
   HIPCHK(hipMalloc(&h->dmodel, sizeof(MData)));
   HIPCHK(hipMemcpy(h->dmodel, md.get(), sizeof(MData), hipMemcpyHostToDevice));
   h->m.d = (const MData*)h->dmodel;
-  HIPCHK(hipMalloc((void**)&h->m.jspill, (size_t)n_envs * JSPILL * sizeof(float)));
+  // fast tier: one spill block per workgroup of k_reset / k_set_state (one per env)
+  HIPCHK(hipMalloc((void**)&h->m.jspill, (size_t)n_envs * JSPILL_FAST * sizeof(float)));
   HIPCHK(hipMalloc(&h->dmhdr, sizeof(DModel) + sizeof(DState)));
-  HIPCHK(hipMalloc((void**)&h->next_env, 8 * sizeof(int)));
+  HIPCHK(hipMalloc((void**)&h->next_env, (10 + (size_t)n_envs) * sizeof(int)));
+  HIPCHK(hipMemset(h->next_env, 0, (10 + (size_t)n_envs) * sizeof(int)));
+  // wide tier: its persistent grid and one spill block per wide workgroup
+#define CALL(TT) (h->wide_grid = std::min(n_envs, wide_ops<TT>()->slots(device)))
+  DISPATCH_TASK(h->m.task_kind, CALL)
+#undef CALL
+  HIPCHK(hipMalloc((void**)&h->jspill_wide, (size_t)h->wide_grid * JSPILL_WIDE * sizeof(float)));
+  HIPCHK(hipMalloc(&h->dmhdr_wide, sizeof(DModel) + sizeof(DState)));
   const size_t bytes = layout_state(h.get(), nullptr);   // dry run: sizes only
   HIPCHK(hipMalloc(&h->dstate, bytes));
   HIPCHK(hipMemset(h->dstate, 0, bytes));
@@ -1357,7 +1546,8 @@ int aw_dims(const aw_handle* h, int* d) {
   if (!h || !d) return fail(AW_EINVAL, "aw_dims: null");
   const DModel& m = h->m;
   int v[AW_NDIMS] = {m.nq, m.nv, m.nu, m.obs_dim, m.nparam, m.frame_skip, m.horizon, m.task_kind, h->nenv,
-                     m.nbody, m.nsite, m.ngeom, m.npairall, MAXCON, MAXEFC, MAXDENSE, std::min(h->slots, h->nenv)};
+                     m.nbody, m.nsite, m.ngeom, m.npairall, NCONMAX, NJMAX, WIDE_MAXDENSE, std::min(h->slots, h->nenv),
+                     FAST_MAXCON, 64 * FAST_NRL, FAST_MAXDENSE, h->wide_grid};
   memcpy(d, v, sizeof(v));
   return AW_OK;
 }
@@ -1371,6 +1561,14 @@ int aw_set_option(aw_handle* h, int disableflags, int iterations, int noslip_ite
   if (noslip_iterations >= 0) h->m.noslip_iterations = noslip_iterations;
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipDeviceSynchronize());   // steps already queued on any stream read the old header
+  return upload_header(h);
+}
+
+int aw_set_tier(aw_handle* h, int mode) {
+  if (!h || mode < 0 || mode > 1) return fail(AW_EINVAL, "aw_set_tier: mode must be 0 (automatic) or 1 (wide only)");
+  h->m.force_wide = mode;
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipDeviceSynchronize());   // queued launches read the old header
   return upload_header(h);
 }
 

@@ -22,23 +22,66 @@ constexpr int MAXG = 36;      // collidable geoms (compact list)
 constexpr int MAXS = 32;      // sites
 constexpr int MAXT = 44;      // tendons
 constexpr int MAXU = 30;      // actuators
-// Constraint capacities.  Sized from the oracle's work counts at MuJoCo's own capacities
-// (nconmax 100 / njmax 500, DAPG_assets.xml:4) under the reference's pretrained DAPG policies
-// (profiles/work_counts_*_dapg.json: max ncon 20, nefc 130, dense rows 98 over 4 tasks x 32
-// envs x one horizon): 2.4x / 1.5x / 1.3x headroom.  Overflow still raises ST_*_OVERFLOW.
+// Constraint capacities: the fast / wide tiers below.  The fast tier's were sized from the
+// oracle's work counts at MuJoCo's own capacities (nconmax 100 / njmax 500, DAPG_assets.xml:4)
+// under the reference's pretrained DAPG policies (profiles/work_counts_*_dapg.json: max ncon 20,
+// nefc 130, dense rows 98 over 4 tasks x 32 envs x one horizon).
 constexpr int MAXJB = 6;      // joints of one body (the free objects' 3 slides + 3 hinges)
-constexpr int MAXCON = 48;    // contacts per env (one lane each in the sort)
-constexpr int NRL = 3;        // constraint rows per lane in the Newton solver
-constexpr int MAXEFC = 64 * NRL;  // constraint rows (192)
-constexpr int MAXDENSE = 128; // dense (contact) rows: noslip keeps <= 64 opposing edge pairs, one per lane
-constexpr int JL = 32;        // dense J rows kept in LDS; rows [JL, MAXDENSE) live in the env's global
-                              // spill block (DModel::jspill), read back through L1 / L2
-constexpr int JSPILL = (MAXDENSE - JL) * VS;  // floats per env in the spill block (row stride VS)
 constexpr int MAXP = 8;       // per-env model parameters
 constexpr int MAXLEV = 16;    // kinematic tree depth
 constexpr int MAXTOUCH = 4;   // task touch sensors
 constexpr int MAXPAIRCON = 8; // contacts per geom pair
 constexpr int NCLASS = 5;      // collider classes: plane-*, round-round, round-box, box-box, MPR
+
+}  // namespace aw
+
+// ---------------------------------------------------------------------------------------
+// Two capacity tiers, one source.  The FAST tier (k_step, two waves per SIMD) holds the
+// constraint sizes above, which cover all but ~1e-5 of env-steps (relocate's random-action tail
+// reaches 126 dense rows in 1 024 envs x 200 steps, tools/capacity_tail.py).  An env-step that
+// needs more is not truncated: the fast tier abandons it before writing anything and queues it
+// for the WIDE tier (k_step_wide, the same code compiled with -DAW_WIDE), which holds MuJoCo's
+// own capacities -- nconmax 100 contacts and njmax 500 constraint rows (DAPG_assets.xml:4) -- and
+// re-runs the env-step from its unchanged pre-step state.  So the only constraints ever dropped
+// are the ones MuJoCo drops, with its ST_*_OVERFLOW flags.  Every Env-dependent definition lives in
+// a per-tier inline namespace, so the two translation units that instantiate the same functions
+// with different capacities never share a (mangled) name.
+namespace aw {
+constexpr int FAST_MAXCON = 48, FAST_NRL = 3, FAST_MAXDENSE = 128;
+constexpr int WIDE_MAXCON = 100, WIDE_NRL = 8, WIDE_MAXDENSE = 500;
+constexpr int NCONMAX = 100, NJMAX = 500;   // the reference model's caps (DAPG_assets.xml:4)
+#ifdef AW_WIDE
+inline namespace wide {
+constexpr bool WIDE = true;
+constexpr int MAXCON = WIDE_MAXCON;   // contacts per env (64 per chunk in the lane-per-contact stages)
+constexpr int NRL = WIDE_NRL;         // constraint rows per lane in the Newton solver
+constexpr int EFC_CAP = NJMAX;        // rows kept (MuJoCo's njmax), storage MAXEFC >= EFC_CAP
+constexpr int MAXDENSE = WIDE_MAXDENSE;
+#else
+inline namespace fast {
+constexpr bool WIDE = false;
+constexpr int MAXCON = FAST_MAXCON;   // contacts per env (one lane each in the sort)
+constexpr int NRL = FAST_NRL;         // constraint rows per lane in the Newton solver
+constexpr int EFC_CAP = 64 * FAST_NRL;
+constexpr int MAXDENSE = FAST_MAXDENSE;  // dense (contact) rows
+#endif
+constexpr int MAXEFC = 64 * NRL;      // constraint rows (fast 192, wide 512)
+constexpr int NCH = (MAXCON + 63) / 64;      // 64-contact chunks of the lane-per-contact stages
+constexpr int NDCH = (MAXDENSE + 63) / 64;   // 64-row chunks of the dense rows (noslip pair scan)
+constexpr int JL = 32;        // dense J rows kept in LDS; rows [JL, MAXDENSE) live in the env's global
+                              // spill block (DModel::jspill), read back through L1 / L2
+constexpr int JSPILL = (MAXDENSE - JL) * VS;  // floats per slot in the spill block (row stride VS)
+static_assert(EFC_CAP <= MAXEFC && MAXDENSE <= EFC_CAP, "constraint capacities");
+}  // inline namespace
+}  // namespace aw
+
+namespace aw {
+constexpr int JSPILL_FAST = (FAST_MAXDENSE - 32) * VS, JSPILL_WIDE = (WIDE_MAXDENSE - 32) * VS;
+#ifdef AW_WIDE
+#define AW_TIER wide
+#else
+#define AW_TIER fast
+#endif
 
 constexpr float MINVAL = 1e-15f;
 
@@ -93,7 +136,8 @@ enum {
   DSBL_ACTUATION = 1 << 10, DSBL_REFSAFE = 1 << 11, DSBL_SENSOR = 1 << 12, DSBL_NOSLIP = 1 << 14,
   DSBL_EULERDAMP = 1 << 15,
 };
-enum { ST_BADQPOS = 1, ST_BADQVEL = 2, ST_BADQACC = 4, ST_CON_OVERFLOW = 8, ST_EFC_OVERFLOW = 16 };
+// ST_WIDE: the env-step (or reset / set_state forward) ran in the wide tier (informational)
+enum { ST_BADQPOS = 1, ST_BADQVEL = 2, ST_BADQACC = 4, ST_CON_OVERFLOW = 8, ST_EFC_OVERFLOW = 16, ST_WIDE = 32 };
 
 // ---------------------------------------------------------------------------------------
 // Device model.  Every per-object array sits at a compile-time offset inside ONE read-only
@@ -203,8 +247,9 @@ struct DModel {
   double mpr_tolerance64;
   int cls_start[NCLASS + 1];  // collider class c owns pair-list slots [cls_start[c], cls_start[c+1])
   int nrgeom;                 // rendered geoms
+  int force_wide;             // test hook (aw_set_tier): every forward of the fast tier defers to the wide tier
   const MData* __restrict__ d;
-  float* jspill;              // per-env dense-J overflow rows [nenv][JSPILL] (device)
+  float* jspill;              // dense-J rows past JL, one block of the tier's JSPILL floats per workgroup slot (device)
   unsigned long long env_offset;   // global id of env 0 of this handle (shards): Philox keys
 };
 
@@ -224,6 +269,7 @@ struct DModel {
 __host__ __device__ constexpr int tri(int j) { return 4 * (j + 2 * (j / 4) * (j / 4 - 1) + (j % 4) * (j / 4)); }
 constexpr int NPACK = tri(MAXV);
 
+inline namespace AW_TIER {   // Env-dependent definitions: per capacity tier
 struct __attribute__((aligned(16))) Env {
   union {
     struct {  // phase K
@@ -289,6 +335,8 @@ static_assert(KIN64_SC_OFF + MAXV * KIN64_SC_W * 8 <= JL * VS * 4, "fp64 joint r
 AW_DEV double* kin64_sc(Env& s, int j) {
   return reinterpret_cast<double*>(reinterpret_cast<char*>(&s.J[0][0]) + KIN64_SC_OFF) + KIN64_SC_W * j;
 }
+
+}  // inline namespace AW_TIER
 
 // ---------------------------------------------------------------------------------------
 // wave primitives

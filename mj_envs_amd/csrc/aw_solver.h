@@ -287,7 +287,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
     for (int side = 0; side < 2; side++) {
       if (!(side ? hi : lo)) continue;
       int r = off++;
-      if (r >= MAXEFC) { atomicOr(&s.status, (unsigned)ST_EFC_OVERFLOW); continue; }
+      if (r >= EFC_CAP) { atomicOr(&s.status, (unsigned)ST_EFC_OVERFLOW); continue; }
       s.efc_type[r] = C_LIM_JNT; s.efc_id[r] = lane;
       s.efc_i0[r] = lane; s.efc_i1[r] = -1; s.efc_v0[r] = side ? -1.f : 1.f; s.efc_v1[r] = 0.f;
       s.rowbuf[r] = side ? dhi : dlo; s.efc_floss[r] = 0.f; s.efc_force[r] = MD(dof_invweight0, lane);
@@ -312,7 +312,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
     for (int side = 0; side < 2; side++) {
       if (!(side ? hi : lo)) continue;
       int r = off++;
-      if (r >= MAXEFC) { atomicOr(&s.status, (unsigned)ST_EFC_OVERFLOW); continue; }
+      if (r >= EFC_CAP) { atomicOr(&s.status, (unsigned)ST_EFC_OVERFLOW); continue; }
       float sg = side ? -1.f : 1.f;
       s.efc_type[r] = C_LIM_TEN; s.efc_id[r] = lane;
       s.efc_i0[r] = MD(ten_d0, lane); s.efc_i1[r] = MD(ten_d1, lane);
@@ -321,80 +321,93 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
     }
   }
   int nsparse = nfl + njl + ntl;
-  if (nsparse > MAXEFC) nsparse = MAXEFC;
-  // contacts: dense rows
-  int ncon = s.ncon;
-  int dim = 0, nr = 0, pair = 0;
-  if (lane < ncon) {
-    pair = s.con_pair[lane];
-    dim = MD(cp_condim, pair);
-    nr = dim == 1 ? 1 : 2 * (dim - 1);
-  }
-  int ntot;
+  if (nsparse > EFC_CAP) nsparse = EFC_CAP;
+  // contacts: dense rows, lane = contact in chunks of 64 (one chunk in the fast tier).  A contact
+  // is kept only if its rows fit: the row offsets are prefix sums, so the kept contacts are a
+  // prefix of the list (mj_makeConstraint stops at the first one that does not fit).
+  const int ncon = s.ncon;
+  int nd = 0, dbase = 0;
+  int c_dim[NCH], c_pair[NCH], c_r0[NCH];
   static_assert(2 * (6 - 1) < 16, "rows per contact (condim <= 6) fit the scan's 4 bits");
-  int doff = wave_excl_scan<4>(nr, lane, &ntot);
-  bool inc = lane < ncon && doff + nr <= MAXDENSE && nsparse + doff + nr <= MAXEFC;
-  int nd = 0;
-  {
-    int cand = inc ? doff + nr : 0;
-    nd = (int)wave_max((float)cand);
-  }
-  if (lane < ncon && !inc) atomicOr(&s.status, (unsigned)ST_EFC_OVERFLOW);
-  if (lane < ncon) s.con_efc[lane] = inc ? nsparse + doff : -1;
-  if (inc) {
-    const float tran = MD(cp_tran, pair), rot = MD(cp_rot, pair);
-    float pm = s.con_dist[lane] - (MD(cp_margin, pair) - MD(cp_gap, pair));
-    int r = nsparse + doff;
-    if (dim == 1) {
-      s.efc_type[r] = C_CON_FRICTIONLESS; s.efc_id[r] = lane; s.rowbuf[r] = pm; s.efc_floss[r] = 0.f;
-      s.efc_force[r] = tran; s.efc_i0[r] = 0; s.efc_i1[r] = 0;
-    } else {
-      for (int k = 1; k < dim; k++) {
-        float fri = MD(cp_friction, 5 * pair + k - 1);
-        float dA = tran + fri * fri * (k < 3 ? tran : rot);
-        for (int sd = 0; sd < 2; sd++) {
-          s.efc_type[r] = C_CON_PYRAMIDAL; s.efc_id[r] = lane; s.rowbuf[r] = pm; s.efc_floss[r] = 0.f;
-          s.efc_force[r] = dA; s.efc_i0[r] = k; s.efc_i1[r] = sd ? -1 : 1;
-          r++;
+#pragma unroll
+  for (int h = 0; h < NCH; h++) {
+    const int c = lane + 64 * h;
+    int dim = 0, nr = 0, pair = 0;
+    if (c < ncon) {
+      pair = s.con_pair[c];
+      dim = MD(cp_condim, pair);
+      nr = dim == 1 ? 1 : 2 * (dim - 1);
+    }
+    int ntot;
+    const int doff = dbase + wave_excl_scan<4>(nr, lane, &ntot);
+    dbase += ntot;
+    const bool inc = c < ncon && doff + nr <= MAXDENSE && nsparse + doff + nr <= EFC_CAP;
+    {
+      const int cand = inc ? doff + nr : 0;
+      const int ndh = (int)wave_max((float)cand);
+      nd = h == 0 ? ndh : (ndh > nd ? ndh : nd);
+    }
+    if (c < ncon && !inc) atomicOr(&s.status, (unsigned)ST_EFC_OVERFLOW);
+    if (c < ncon) s.con_efc[c] = inc ? nsparse + doff : -1;
+    if (inc) {
+      const float tran = MD(cp_tran, pair), rot = MD(cp_rot, pair);
+      float pm = s.con_dist[c] - (MD(cp_margin, pair) - MD(cp_gap, pair));
+      int r = nsparse + doff;
+      if (dim == 1) {
+        s.efc_type[r] = C_CON_FRICTIONLESS; s.efc_id[r] = c; s.rowbuf[r] = pm; s.efc_floss[r] = 0.f;
+        s.efc_force[r] = tran; s.efc_i0[r] = 0; s.efc_i1[r] = 0;
+      } else {
+        for (int k = 1; k < dim; k++) {
+          float fri = MD(cp_friction, 5 * pair + k - 1);
+          float dA = tran + fri * fri * (k < 3 ? tran : rot);
+          for (int sd = 0; sd < 2; sd++) {
+            s.efc_type[r] = C_CON_PYRAMIDAL; s.efc_id[r] = c; s.rowbuf[r] = pm; s.efc_floss[r] = 0.f;
+            s.efc_force[r] = dA; s.efc_i0[r] = k; s.efc_i1[r] = sd ? -1 : 1;
+            r++;
+          }
         }
       }
     }
+    c_dim[h] = dim; c_pair[h] = pair; c_r0[h] = inc ? nsparse + doff : -1;
   }
   if (lane == 0) { s.nsparse = nsparse; s.ndense = nd; s.nefc = nsparse + nd; }
   wsync();
   AW_PROF(s, PR_CS_SPARSE);
-  // dense J rows.  The per-contact model data is gathered first with lane = contact (one round of
-  // loads).
-  unsigned long long c_m1 = 0ull, c_m2 = 0ull;
-  int c_root1 = 0, c_root2 = 0;
-  float c_f0 = 0.f, c_f1 = 0.f;
-  if (lane < ncon) {
-    c_m1 = MD(cp_mask1, pair); c_m2 = MD(cp_mask2, pair);
-    c_root1 = MD(cp_root1, pair); c_root2 = MD(cp_root2, pair);
-    c_f0 = MD(cp_friction, 5 * pair); c_f1 = MD(cp_friction, 5 * pair + 1);
-  }
-  const int c_pair = pair, c_dim = dim, c_r0 = lane < ncon ? s.con_efc[lane] : -1;
-  {
+  // dense J rows, one contact chunk at a time.  The chunk's per-contact model data is gathered
+  // first with lane = contact (one round of loads).
+#pragma unroll
+  for (int h = 0; h < NCH; h++) {
+    const int cb = 64 * h;
+    unsigned long long c_m1 = 0ull, c_m2 = 0ull;
+    int c_root1 = 0, c_root2 = 0;
+    float c_f0 = 0.f, c_f1 = 0.f;
+    if (lane + cb < ncon) {
+      const int pair = c_pair[h];
+      c_m1 = MD(cp_mask1, pair); c_m2 = MD(cp_mask2, pair);
+      c_root1 = MD(cp_root1, pair); c_root2 = MD(cp_root2, pair);
+      c_f0 = MD(cp_friction, 5 * pair); c_f1 = MD(cp_friction, 5 * pair + 1);
+    }
     // (contact, dof) work items flattened over the wave: ceil(ncon NV / 64) passes instead of one
     // per contact (hammer: 33 of 64 lanes busy per contact before); each lane takes its contact's
     // data from the contact's lane by a bpermute.  Same arithmetic per entry (r04w A/B: -1.5 %
     // DAPG, -0.3 % random)
-    const int nlead = __popcll(__ballot(lane < ncon && c_r0 >= 0));   // contacts before any overflow
+    const int nlead = __popcll(__ballot(c_r0[h] >= 0));   // the chunk's kept contacts (a prefix)
     const int total = nlead * NV;
     for (int base = 0; base < total; base += 64) {
       const int w = base + lane;
       const bool act = w < total;
-      const int c = act ? w / NV : 0;
-      const int k = act ? w - c * NV : 0;
-      const int r0 = __shfl(c_r0, c, 64);
-      const int pr = __shfl(c_pair, c, 64);
-      const int cdim = __shfl(c_dim, c, 64);
-      const unsigned long long m1 = ((unsigned long long)(unsigned)__shfl((int)(c_m1 >> 32), c, 64) << 32) |
-                                    (unsigned)__shfl((int)c_m1, c, 64);
-      const unsigned long long m2 = ((unsigned long long)(unsigned)__shfl((int)(c_m2 >> 32), c, 64) << 32) |
-                                    (unsigned)__shfl((int)c_m2, c, 64);
-      const int root1 = __shfl(c_root1, c, 64), root2 = __shfl(c_root2, c, 64);
-      const float f0 = __shfl(c_f0, c, 64), f1 = __shfl(c_f1, c, 64);
+      const int cl = act ? w / NV : 0;
+      const int k = act ? w - cl * NV : 0;
+      const int c = cb + cl;
+      const int r0 = __shfl(c_r0[h], cl, 64);
+      const int pr = __shfl(c_pair[h], cl, 64);
+      const int cdim = __shfl(c_dim[h], cl, 64);
+      const unsigned long long m1 = ((unsigned long long)(unsigned)__shfl((int)(c_m1 >> 32), cl, 64) << 32) |
+                                    (unsigned)__shfl((int)c_m1, cl, 64);
+      const unsigned long long m2 = ((unsigned long long)(unsigned)__shfl((int)(c_m2 >> 32), cl, 64) << 32) |
+                                    (unsigned)__shfl((int)c_m2, cl, 64);
+      const int root1 = __shfl(c_root1, cl, 64), root2 = __shfl(c_root2, cl, 64);
+      const float f0 = __shfl(c_f0, cl, 64), f1 = __shfl(c_f1, cl, 64);
       if (act) {
         const float* pos = s.con_pos[c];
         float fr[9];
@@ -475,27 +488,8 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
 #endif
 constexpr float NT_NOISE_DOF = AW_NT_NOISE_DOF;
 // why the Newton solve stopped (s.it_newton = iterations + 1000 * reason, aw_forward_dump)
-enum { NT_EXIT_MAXITER = 0, NT_EXIT_NOSTEP = 1, NT_EXIT_NOISE = 2, NT_EXIT_IMPROVE = 3, NT_EXIT_GRAD = 4 };
-#ifndef AW_NSP_CACHE
-#define AW_NSP_CACHE 16
-#endif
-constexpr int NSP_CACHE = AW_NSP_CACHE;   // noslip edge pairs whose jd / xd rows stay in VGPRs
-// noslip edge pairs past the VGPR cache park their rows (jd = J_e - J_e+1 and xd = inv(M) jd', two
-// dof vectors: only lanes < MAXV carry them, 2 * MAXV floats per pair) in LDS that is dead during
-// the PGS sweeps: the phase-K / phase-S union at the start of Env (the factor of M was consumed
-// by inv(M)), then efc_D and rowbuf (written again only after noslip).
-constexpr int XPS = 2 * MAXV;
-constexpr int NSP_UNION = (int)(offsetof(Env, qpos) / (XPS * sizeof(float)));
-constexpr int NSP_ROWS = MAXEFC / XPS;          // slots in each of efc_D and rowbuf
-// KEEP_D (aw_forward_dump's k_dump): efc_D is reported after the solve, so it is not parked in
-template <bool KEEP_D> constexpr int NSP_LDS = NSP_UNION + (KEEP_D ? 1 : 2) * NSP_ROWS;
-template <bool KEEP_D>
-AW_DEV float* xpark_slot(Env& s, int q) {
-  if (q < NSP_UNION) return reinterpret_cast<float*>(&s) + q * XPS;
-  q -= NSP_UNION;
-  if (KEEP_D) return s.rowbuf + q * XPS;
-  return q < NSP_ROWS ? s.efc_D + q * XPS : s.rowbuf + (q - NSP_ROWS) * XPS;
-}
+// NT_EXIT_NOROWS: no constraint rows, no Newton solve (forward's default before the solver runs)
+enum { NT_EXIT_MAXITER = 0, NT_EXIT_NOSTEP = 1, NT_EXIT_NOISE = 2, NT_EXIT_IMPROVE = 3, NT_EXIT_GRAD = 4, NT_EXIT_NOROWS = 5 };
 struct RowR {
   float D, floss, Jaref, Jp, force;
   int st, fr, valid;
@@ -942,26 +936,32 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
   // jd . qacc in-lane, no wave reductions on the scan).  A pair with K < MINVAL keeps its lane but
   // is inert (ca = cb = 0: its update is exactly zero).  Pairs past NPL keep their constants in
   // lane p - NPL.
-  unsigned long long cmask[2];
+  unsigned long long cmask[NDCH];
 #pragma unroll
-  for (int h = 0; h < 2; h++) {
+  for (int h = 0; h < NDCH; h++) {
     const int e = lane + 64 * h;
     bool c = e + 1 < ndense;
     if (c) c = s.efc_type[nsparse + e] == C_CON_PYRAMIDAL && s.efc_i1[nsparse + e] == 1;
     cmask[h] = __ballot(c);
   }
   int npr = 0;
-  int ex_e = 0;
-  float ex_ca = 0.f, ex_cb = 0.f, ex_K = 0.f, ex_fa = 0.f, ex_fb = 0.f;
+  // pairs past the lanes: pair NPL + 64 xc + l keeps its constants in lane l of chunk xc
+  constexpr int NXCH = (MAXDENSE / 2 - NPL + 63) / 64 > 0 ? (MAXDENSE / 2 - NPL + 63) / 64 : 1;
+  int ex_e[NXCH];
+  float ex_ca[NXCH], ex_cb[NXCH], ex_K[NXCH], ex_fa[NXCH], ex_fb[NXCH];
+#pragma unroll
+  for (int xc = 0; xc < NXCH; xc++) { ex_e[xc] = 0; ex_ca[xc] = ex_cb[xc] = ex_K[xc] = ex_fa[xc] = ex_fb[xc] = 0.f; }
   // with >= 4 pair lanes the lane pairs' xd = inv(M) jd' come from one MFMA product below
   // (DAPG +2.7 %, random +-0, r03zg, against per-pair VALU products)
-  const int npr_all = __popcll(cmask[0]) + __popcll(cmask[1]);
+  int npr_all = 0;
+#pragma unroll
+  for (int h = 0; h < NDCH; h++) npr_all += __popcll(cmask[h]);
   // (hammer; relocate's 36 x 36 inv(M) does not fit the staging area, door / pen have 34 pair lanes)
   // the staging writes NV rows of inv(M) and the product writes rows p < 32 of the buffer
   constexpr bool X_FIT = NPL <= 32 && (NV > 32 ? NV : 32) * XS * sizeof(float) <= offsetof(Env, qpos);
   const bool x_mfma = X_FIT && (npr_all < NPL ? npr_all : NPL) >= 4;
 #pragma unroll
-  for (int h = 0; h < 2; h++) {
+  for (int h = 0; h < NDCH; h++) {
     unsigned long long mk = cmask[h];
     while (mk) {
       const int e = 64 * h + __builtin_ctzll(mk);
@@ -981,11 +981,14 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
         const bool ok = K >= MINVAL;
         const float ik = ok ? 1.0f / K : 0.f;
         const float ard = s.efc_aref[nsparse + e] - s.efc_aref[nsparse + e + 1];
-        if (lane == p - NPL) {
-          ex_e = e; ex_ca = ik; ex_cb = ard * ik; ex_K = ok ? K : 0.f;
-          ex_fa = s.efc_force[nsparse + e];
-          ex_fb = s.efc_force[nsparse + e + 1];
-        }
+        const int x = p - NPL;
+#pragma unroll
+        for (int xc = 0; xc < NXCH; xc++)
+          if (xc == (x >> 6) && lane == (x & 63)) {
+            ex_e[xc] = e; ex_ca[xc] = ik; ex_cb[xc] = ard * ik; ex_K[xc] = ok ? K : 0.f;
+            ex_fa[xc] = s.efc_force[nsparse + e];
+            ex_fb[xc] = s.efc_force[nsparse + e + 1];
+          }
       }
     }
   }
@@ -1236,17 +1239,21 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
     fa += d;
     fb -= d;
     // pairs past the lanes: their column of A rebuilt, the residual by a wave reduction
-    for (int x = 0; x < npr - NPL; x++) {
-      const int e = rlane_i(ex_e, x);
-      float jd, col;
-      pair_col(e, jd, col);
-      const float y = fmaf(-wave_sum(jd * R), rlane(ex_ca, x), rlane(ex_cb, x));
-      const float d1 = __builtin_amdgcn_fmed3f(y, -rlane(ex_fa, x), rlane(ex_fb, x));
-      R = fmaf(col, d1, R);
-      if (lane == x) {
-        imp += ex_K * d1 * (0.5f * d1 - y);
-        ex_fa += d1;
-        ex_fb -= d1;
+#pragma unroll
+    for (int xc = 0; xc < NXCH; xc++) {
+      const int nx = npr - NPL - 64 * xc;
+      for (int x = 0; x < (nx < 64 ? nx : 64); x++) {
+        const int e = rlane_i(ex_e[xc], x);
+        float jd, col;
+        pair_col(e, jd, col);
+        const float y = fmaf(-wave_sum(jd * R), rlane(ex_ca[xc], x), rlane(ex_cb[xc], x));
+        const float d1 = __builtin_amdgcn_fmed3f(y, -rlane(ex_fa[xc], x), rlane(ex_fb[xc], x));
+        R = fmaf(col, d1, R);
+        if (lane == x) {
+          imp += ex_K[xc] * d1 * (0.5f * d1 - y);
+          ex_fa[xc] += d1;
+          ex_fb[xc] -= d1;
+        }
       }
     }
     if (-wave_sum(imp) * scale < m.noslip_tolerance) break;
@@ -1258,10 +1265,12 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
     s.efc_force[nsparse + rowe] = fa;
     s.efc_force[nsparse + rowe + 1] = fb;
   }
-  if (lane < npr - NPL) {
-    s.efc_force[nsparse + ex_e] = ex_fa;
-    s.efc_force[nsparse + ex_e + 1] = ex_fb;
-  }
+#pragma unroll
+  for (int xc = 0; xc < NXCH; xc++)
+    if (lane + 64 * xc < npr - NPL) {
+      s.efc_force[nsparse + ex_e[xc]] = ex_fa[xc];
+      s.efc_force[nsparse + ex_e[xc] + 1] = ex_fb[xc];
+    }
   wsync();
 }
 
@@ -1327,22 +1336,26 @@ AW_DEV void stage_touch(const DModel& m, Env& s, int lane) {
   for (int t = 0; t < m.ntouch; t++) {
     int site = MD(touch_site, t), bid = MD(site_bodyid, site);
     float val = 0.f;
-    if (lane < s.ncon && s.con_efc[lane] >= 0 && !(m.disableflags & DSBL_SENSOR)) {
-      int pr = s.con_pair[lane];
-      int b1 = MD(geom_bodyid, MD(cp_g1, pr)), b2 = MD(geom_bodyid, MD(cp_g2, pr));
-      if (bid == b1 || bid == b2) {
-        int adr = s.con_efc[lane], dim = MD(cp_condim, pr);
-        float fn = 0.f;
-        if (dim == 1) fn = s.efc_force[adr];
-        else for (int j = 0; j < 2 * (dim - 1); j++) fn += s.efc_force[adr + j];
-        if (fn > 0.f) {
-          float ray[3];
-          copy3(ray, s.con_nrm[lane]);
-          normalize3(ray);
-          if (bid == b2) scl3(ray, ray, -1.f);
-          float tsz[3] = {MD(touch_size, 3 * t), MD(touch_size, 3 * t + 1), MD(touch_size, 3 * t + 2)};
-          if (ray_geom(s.sxpos[site], s.txmat[t], tsz, s.con_pos[lane], ray, MD(touch_type, t)) >= 0.f)
-            val = fn;
+#pragma unroll
+    for (int h = 0; h < NCH; h++) {
+      const int c = lane + 64 * h;
+      if (c < s.ncon && s.con_efc[c] >= 0 && !(m.disableflags & DSBL_SENSOR)) {
+        int pr = s.con_pair[c];
+        int b1 = MD(geom_bodyid, MD(cp_g1, pr)), b2 = MD(geom_bodyid, MD(cp_g2, pr));
+        if (bid == b1 || bid == b2) {
+          int adr = s.con_efc[c], dim = MD(cp_condim, pr);
+          float fn = 0.f;
+          if (dim == 1) fn = s.efc_force[adr];
+          else for (int j = 0; j < 2 * (dim - 1); j++) fn += s.efc_force[adr + j];
+          if (fn > 0.f) {
+            float ray[3];
+            copy3(ray, s.con_nrm[c]);
+            normalize3(ray);
+            if (bid == b2) scl3(ray, ray, -1.f);
+            float tsz[3] = {MD(touch_size, 3 * t), MD(touch_size, 3 * t + 1), MD(touch_size, 3 * t + 2)};
+            if (ray_geom(s.sxpos[site], s.txmat[t], tsz, s.con_pos[c], ray, MD(touch_type, t)) >= 0.f)
+              val += fn;
+          }
         }
       }
     }

@@ -133,6 +133,58 @@ int or_step(void* p, int n, const double* params, const double* action, double* 
   return 0;
 }
 
+/* or_step + per-env work counts of the env-step (test / profiling hook, tools/work_counts.py):
+ * stats[e][8] = max ncon, max nefc, max dense (contact) rows over the frame_skip substeps, summed
+ * Newton iterations, line-search derivative evaluations and noslip sweeps, substeps, status */
+int or_step_stats(void* p, int n, const double* params, const double* action, double* qpos, double* qvel,
+                  double* warm, double* obs, double* reward, uint8_t* done, uint8_t* goal, int32_t* stats,
+                  int nthreads) {
+  const Model* m = &((Handle*)p)->m;
+  int P = m->task_nparam, O = m->task_obs_dim;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel
+#endif
+  {
+    Data d;
+    init_data(m, &d);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 4)
+#endif
+    for (int e = 0; e < n; e++) {
+      apply_params(m, &d, params ? params + (size_t)e * P : nullptr);
+      load_state(m, &d, qpos + (size_t)e * m->nq, qvel + (size_t)e * m->nv, warm ? warm + (size_t)e * m->nv : nullptr);
+      d.status = 0;
+      const double* a = action + (size_t)e * m->nu;
+      for (int i = 0; i < m->nu; i++) {
+        double x = a[i] < -1.0 ? -1.0 : (a[i] > 1.0 ? 1.0 : a[i]);
+        d.ctrl[i] = m->task_act_mid[i] + x * m->task_act_rng[i];
+      }
+      int32_t* st = stats + (size_t)e * 8;
+      for (int k = 0; k < 8; k++) st[k] = 0;
+      for (int k = 0; k < m->task_frame_skip; k++) {
+        step(m, &d);
+        int nd = 0;
+        for (int i = 0; i < d.nefc; i++) nd += d.efc_type[i] >= CNSTR_CONTACT_FRICTIONLESS;
+        st[0] = d.ncon > st[0] ? d.ncon : st[0];
+        st[1] = d.nefc > st[1] ? d.nefc : st[1];
+        st[2] = nd > st[2] ? nd : st[2];
+        st[3] += d.solver_iter; st[4] += d.ls_iter; st[5] += d.noslip_iter; st[6] += 1;
+      }
+      st[7] = (int32_t)d.status;
+      store_state(m, &d, qpos + (size_t)e * m->nq, qvel + (size_t)e * m->nv, warm ? warm + (size_t)e * m->nv : nullptr);
+      if (obs) task_obs(m, &d, obs + (size_t)e * O);
+      double r;
+      uint8_t dn, gl;
+      task_reward(m, &d, &r, &dn, &gl, 0);
+      if (reward) reward[e] = r;
+      if (done) done[e] = dn;
+      if (goal) goal[e] = gl;
+    }
+  }
+  return 0;
+}
+
 /* ---- single-env introspection --------------------------------------------------------- */
 int or_forward1(void* p, const double* params, const double* qpos, const double* qvel,
                 const double* warm, const double* ctrl) {
@@ -186,7 +238,8 @@ int or_get1(void* p, const char* name, double* out, int cap) {
   }
   std::vector<double> tmp;
   if (s == "scalars") {
-    tmp = {(double)d->ncon, (double)d->nefc, (double)d->solver_iter, (double)d->noslip_iter, (double)d->status};
+    tmp = {(double)d->ncon, (double)d->nefc, (double)d->solver_iter, (double)d->noslip_iter, (double)d->status,
+           (double)d->ls_iter};
   } else if (s == "efc_type") {
     for (int i = 0; i < d->nefc; i++) tmp.push_back(d->efc_type[i]);
   } else if (s == "efc_id") {

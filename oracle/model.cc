@@ -170,7 +170,7 @@ void init_data(const Model* m, Data* d) {
   d->efc_aref.assign(E, 0); d->efc_vel.assign(E, 0); d->efc_force.assign(E, 0);
   d->efc_b.assign(E, 0);
   d->sensordata.assign(m->nsensor, 0);
-  d->solver_iter = d->noslip_iter = 0;
+  d->solver_iter = d->noslip_iter = d->ls_iter = 0;
   d->status = 0;
 }
 

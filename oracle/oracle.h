@@ -129,6 +129,7 @@ struct Data {
       efc_aref, efc_vel, efc_force, efc_b;
   std::vector<num> sensordata;
   int solver_iter, noslip_iter;
+  int ls_iter;          /* line-search derivative evaluations of the last Newton solve (incl. alpha = 0) */
   uint32_t status;
   /* scratch */
   std::vector<num> scratch;

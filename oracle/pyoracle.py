@@ -42,6 +42,8 @@ def lib():
         L.or_reset.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, ctypes.c_int]
         L.or_step.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _u8p,
                               _u8p, _u32p, ctypes.c_int]
+        L.or_step_stats.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _u8p,
+                                    _u8p, ctypes.POINTER(ctypes.c_int32), ctypes.c_int]
         L.or_forward1.argtypes = [ctypes.c_void_p, _dp, _dp, _dp, _dp, _dp]
         L.or_mjstep1.argtypes = [ctypes.c_void_p, _dp, _dp, _dp, _dp, _dp, ctypes.c_int]
         L.or_get1.argtypes = [ctypes.c_void_p, ctypes.c_char_p, _dp, ctypes.c_int]
@@ -110,6 +112,19 @@ class Oracle:
                       _p(state["warm"]), _p(obs), _p(rew), _p(done, _u8p), _p(goal, _u8p),
                       _p(status, _u32p), nthreads)
         return obs, rew, done.astype(bool), goal.astype(bool), status
+
+    def step_stats(self, state: dict, action: np.ndarray, nthreads: int = 0):
+        """step() plus per-env work counts of the env-step: int32 [n, 8] = max ncon, max nefc, max
+        dense rows over the substeps, summed Newton iterations, line-search evaluations, noslip
+        sweeps, substeps, status flags"""
+        n = state["qpos"].shape[0]
+        action = np.ascontiguousarray(action, np.float64).reshape(n, self.nu)
+        obs = np.zeros((n, self.obs_dim)); rew = np.zeros(n)
+        done = np.zeros(n, np.uint8); goal = np.zeros(n, np.uint8); stats = np.zeros((n, 8), np.int32)
+        lib().or_step_stats(self.h, n, _p(state["params"]), _p(action), _p(state["qpos"]), _p(state["qvel"]),
+                            _p(state["warm"]), _p(obs), _p(rew), _p(done, _u8p), _p(goal, _u8p),
+                            stats.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), nthreads)
+        return obs, rew, done.astype(bool), goal.astype(bool), stats
 
     # --- single env ---------------------------------------------------------------------
     def forward1(self, params, qpos, qvel, warm=None, ctrl=None):

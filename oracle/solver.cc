@@ -287,7 +287,7 @@ static void ls_deriv(const Data* d, const NewtonWS& w, num c0, num c1, num alpha
   *d2 = g2;
 }
 
-static num line_search(const Model* m, const Data* d, NewtonWS& w) {
+static num line_search(const Model* m, Data* d, NewtonWS& w) {
   int nv = m->nv;
   mul_M(m, d, w.p.data(), w.Mp.data());
   num c0 = 0, c1 = 0;
@@ -300,6 +300,7 @@ static num line_search(const Model* m, const Data* d, NewtonWS& w) {
   }
   num d1, d2;
   ls_deriv(d, w, c0, c1, 0, &d1, &d2);
+  d->ls_iter++;
   if (d1 >= 0) return 0;
   num tol = 1e-10 * std::fabs(d1);
   num alpha = 0, lo = 0, hi = -1;
@@ -309,6 +310,7 @@ static num line_search(const Model* m, const Data* d, NewtonWS& w) {
     if (an == alpha) break;
     alpha = an;
     ls_deriv(d, w, c0, c1, alpha, &d1, &d2);
+    d->ls_iter++;
     if (d1 < 0) lo = alpha; else hi = alpha;
     if (std::fabs(d1) <= tol) break;
   }
@@ -331,7 +333,7 @@ void contact_force(const Model* m, const Data* d, int c, num* r) {
 
 void fwd_constraint(const Model* m, Data* d) {
   int nv = m->nv, nefc = d->nefc;
-  d->solver_iter = d->noslip_iter = 0;
+  d->solver_iter = d->noslip_iter = d->ls_iter = 0;
   if (!nefc) {
     d->qacc = d->qacc_smooth;
     std::fill(d->qfrc_constraint.begin(), d->qfrc_constraint.end(), 0.0);

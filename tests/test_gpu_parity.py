@@ -159,9 +159,11 @@ def _err_report(label, eq, ev, ok):
 # Error-distribution gates (the per-case tolerance sits orders of magnitude
 # above the achieved error, so a 10x regression could pass it).  Over the (env, step) cases within
 # tolerance, the p50 / p99 of max |dqpos| and max |dqvel| / (1 + |v|) must stay below these bounds,
-# set at ~4x the r04 measurements of the worst task / regime (profiles/r04*_pytest_gpu.txt).
-ERR_P50 = dict(qpos=1e-6, qvel=1e-4)
-ERR_P99 = dict(qpos=1.8e-5, qvel=4e-3)
+# set at ~4x the r04 measurements of the worst task / regime (profiles/r04z8_pytest_gpu.txt: p50
+# qpos 2.0e-7, qvel 1.8e-5; p99 qpos 1.95e-6 (relocate C3), qvel 1.2e-4), so a 10x regression of
+# the median or of the tail fails even when every case stays inside the per-case tolerance.
+ERR_P50 = dict(qpos=8e-7, qvel=8e-5)
+ERR_P99 = dict(qpos=8e-6, qvel=5e-4)
 
 
 def _err_gate(r):
@@ -190,16 +192,16 @@ def _oracle_f32_model(env_id, variation=None):
     return _ORACLE_F32MODEL[key]
 
 
-def _fp32_sensitive(o, params, qpos, qvel, warm, act, env_id=None, variation=None, trials=8, ulps=16, seed=0):
-    """Is the fp64 reference itself unstable at fp32 resolution here?  Re-runs the oracle's
+def _fp32_spread(o, params, qpos, qvel, warm, act, env_id=None, variation=None, trials=8, ulps=16, seed=0):
+    """How far does the fp64 reference itself move at fp32 resolution here?  Re-runs the oracle's
     env-step (a) on the fp32-rounded model the GPU holds and (b) from the same state with every
-    state component perturbed by up to `ulps` fp32 ulps (relative 2^-23 each): True when one of
-    those results leaves the one-step tolerance around the unperturbed fp64 one -- the step sits
-    on a discontinuity (a contact, row state or solver decision switching) or is ill-conditioned
-    within fp32 rounding of its inputs, so an fp32 simulation cannot be held to it.  16 ulps
-    (1.9e-6 relative) is the rounding an fp32 env-step accumulates over its ~10^4 operations per
-    substep; e.g. relocate C3 step 176 env 158 (hand at 26 rad/s): the oracle moves 9e-6 in qpos
-    under 4-ulp inputs and 3.7e-5 under 16 (tolerance 2e-5), the GPU 3.3e-5 (r04h)."""
+    state component perturbed by up to `ulps` fp32 ulps (relative 2^-23 each).  Returns (base,
+    leaves, dq, dv): the unperturbed fp64 result (qpos, qvel), whether one of the runs leaves the
+    one-step tolerance around it, and the largest deviation of any run from it (max |dqpos|, max
+    |dqvel| / (1 + |v|)).  16 ulps (1.9e-6 relative) is the rounding an fp32 env-step accumulates
+    over its ~10^4 operations per substep; e.g. relocate C3 step 176 env 158 (hand at 26 rad/s):
+    the oracle moves 9e-6 in qpos under 4-ulp inputs and 3.7e-5 under 16 (tolerance 2e-5), the
+    GPU 3.3e-5 (r04h)."""
     rng = np.random.default_rng(seed)
     base = dict(qpos=qpos[None].copy(), qvel=qvel[None].copy(), warm=warm[None].copy(), params=params[None].copy())
     o.step(base, act[None])
@@ -213,26 +215,64 @@ def _fp32_sensitive(o, params, qpos, qvel, warm, act, env_id=None, variation=Non
         for k, x in (("qpos", qpos), ("qvel", qvel), ("warm", warm)):
             st[k] = (x * (1 + eps * rng.uniform(-1, 1, x.shape)))[None]
         runs.append((o, st))
+    leaves, dq, dv = False, 0.0, 0.0
     for oo, st in runs:
         oo.step(st, act[None])
-        _, _, ok = _state_err(st["qpos"], st["qvel"], base["qpos"], base["qvel"])
-        if not ok[0]:
-            return True
-    return False
+        eq, ev, ok = _state_err(st["qpos"], st["qvel"], base["qpos"], base["qvel"])
+        leaves |= not ok[0]
+        dq, dv = max(dq, float(eq[0])), max(dv, float(ev[0]))
+    return (base["qpos"][0], base["qvel"][0]), leaves, dq, dv
+
+
+# A miss the fp64 reference cannot resolve at fp32 resolution is explained only if the GPU's own
+# result stays within this multiple of the reference's spread under fp32-size perturbations (a GPU
+# step that is wrong by more than the reference's own instability is not excused by it).
+SPREAD_FACTOR = 4.0
+# Hard cap on every (env, step) case, misses included (NaN fails): a chaotic step may miss the
+# per-case tolerance, but not by a macroscopic amount (1 cm / 10 mrad in qpos in one env-step).
+HARD_CAP = dict(qpos=1e-2, qvel=1.0)
+
+
+def _hard_cap(eq, ev, label):
+    eq, ev = np.asarray(eq, float), np.asarray(ev, float)
+    mq, mv = float(np.max(eq)) if eq.size else 0.0, float(np.max(ev)) if ev.size else 0.0
+    print(f"{label}: max over all cases |dqpos| {mq:.2e}, |dqvel|/(1+|v|) {mv:.2e} "
+          f"(hard cap {HARD_CAP['qpos']:.0e} / {HARD_CAP['qvel']:.0e})")
+    assert mq <= HARD_CAP["qpos"] and mv <= HARD_CAP["qvel"], (label, mq, mv)
+
+
+def _fp32_sensitive(o, params, qpos, qvel, warm, act, env_id=None, variation=None, gpu=None, **kw):
+    """True when the fp64 reference leaves the tolerance under fp32-size perturbations AND (given
+    the GPU's post-step state `gpu` = (qpos, qvel)) the GPU's deviation from the unperturbed fp64
+    result is within SPREAD_FACTOR x the reference's own spread, in qpos and in qvel (or within the
+    tolerance in that quantity)."""
+    (bq, bv), leaves, dq, dv = _fp32_spread(o, params, qpos, qvel, warm, act, env_id, variation, **kw)
+    if not leaves:
+        return False
+    if gpu is None:
+        return True
+    gq, gv = np.asarray(gpu[0], float), np.asarray(gpu[1], float)
+    eq = float(np.abs(gq - bq).max())
+    ev = float((np.abs(gv - bv) / (1 + np.abs(bv))).max())
+    okq = (np.abs(gq - bq) <= 2e-5 + 1e-5 * np.abs(bq)).all() or eq <= SPREAD_FACTOR * dq
+    okv = (np.abs(gv - bv) <= 5e-3 * (1 + np.abs(bv))).all() or ev <= SPREAD_FACTOR * dv
+    return bool(okq and okv)
 
 
 def _classify_misses(env_id, misses, frame_skip, variation=None):
     """every miss must be a discrete event (_discrete_event: the contact / row set differs, or a
     contact sits within fp32 rounding of its margin) or a step the fp64 reference itself cannot
-    resolve at fp32 resolution (_fp32_sensitive): returns the unexplained ones"""
+    resolve at fp32 resolution with the GPU inside that spread (_fp32_sensitive): returns the
+    unexplained ones.  A miss is (step, env, params, qpos, qvel, warm, action[, gpu_qpos, gpu_qvel])."""
     if not misses:
         return []
     o = make_oracle(env_id, variation)[1]
     out = []
-    for (k, e, params, q, v, w, a) in misses:
+    for ms in misses:
+        (k, e, params, q, v, w, a), gpu = ms[:7], (ms[7:9] if len(ms) >= 9 else None)
         if _discrete_event(env_id, variation, o, params, q, v, w, a, frame_skip):
             continue
-        if _fp32_sensitive(o, params, q, v, w, a, env_id, variation):
+        if _fp32_sensitive(o, params, q, v, w, a, env_id, variation, gpu=gpu):
             continue
         out.append((k, e))
     return out
@@ -530,12 +570,13 @@ def _teacher_forced(env_id, disableflags, policy=False, steps=40, n=64):
         torch.cuda.synchronize()
         _, r_ref, _, _, ost = o.step(st, act, nthreads=8)
         ostatus |= int(np.bitwise_or.reduce(ost))
-        eq, ev, ok = _state_err(q.cpu().numpy(), v.cpu().numpy(), st["qpos"], st["qvel"])
+        qg, vg = q.cpu().numpy(), v.cpu().numpy()
+        eq, ev, ok = _state_err(qg, vg, st["qpos"], st["qvel"])
         oks.append(ok)
         eqs.append(eq)
         evs.append(ev)
-        misses += [(k, e, pre["params"][e], pre["qpos"][e], pre["qvel"][e], pre["warm"][e], np.asarray(act[e], np.float64))
-                   for e in np.where(~ok)[0]]
+        misses += [(k, e, pre["params"][e], pre["qpos"][e], pre["qvel"][e], pre["warm"][e], np.asarray(act[e], np.float64),
+                    qg[e].astype(np.float64), vg[e].astype(np.float64)) for e in np.where(~ok)[0]]
         rok.append(_rewards_close(rew.cpu().numpy(), r_ref, check=False))
     frac = np.concatenate(oks).mean()
     rfrac = np.concatenate(rok).mean()
@@ -546,8 +587,10 @@ def _teacher_forced(env_id, disableflags, policy=False, steps=40, n=64):
     label = f"teacher-forced {env_id} (disableflags {disableflags:#x}{', DAPG policy' if policy else ''})"
     print(f"{label}: {frac:.4f} of {n * steps} (env, step) cases within the state tolerance, rewards {rfrac:.4f}")
     err = _err_report(label, np.concatenate(eqs), np.concatenate(evs), np.concatenate(oks))
+    _hard_cap(np.concatenate(eqs), np.concatenate(evs), label)
     unexplained = _classify_misses(env_id, misses, sim.frame_skip)
-    print(f"{label}: {len(misses)} misses, not explained by a discrete event: {unexplained}")
+    print(f"{label}: {len(misses)} misses, not explained by a discrete event or a bounded fp32-sensitive "
+          f"reference: {unexplained}")
     assert not (ostatus & 24), "oracle overflowed MuJoCo's capacities"
     _no_overflow(sim, n)
     assert rfrac >= REWARD_MIN, (env_id, rfrac)
@@ -590,12 +633,14 @@ def test_teacher_forced_headline_config_4096_envs():
         sim.get_state(q, v)
         torch.cuda.synchronize()
         _, r_ref, _, _, _ = o.step(st, act[idx], nthreads=8)
-        eq, ev, okk = _state_err(q.cpu().numpy()[idx], v.cpu().numpy()[idx], st["qpos"], st["qvel"])
+        qg, vg = q.cpu().numpy()[idx], v.cpu().numpy()[idx]
+        eq, ev, okk = _state_err(qg, vg, st["qpos"], st["qvel"])
         oks.append(okk)
         eqs.append(eq)
         evs.append(ev)
         misses += [(k, int(idx[j]), pre["params"][j], pre["qpos"][j], pre["qvel"][j], pre["warm"][j],
-                    np.asarray(act[idx[j]], np.float64)) for j in np.where(~okk)[0]]
+                    np.asarray(act[idx[j]], np.float64), qg[j].astype(np.float64), vg[j].astype(np.float64))
+                   for j in np.where(~okk)[0]]
         roks.append(_rewards_close(rew.cpu().numpy()[idx], r_ref, check=False))
     ok = np.array(oks)
     frac, rfrac = ok.mean(), np.concatenate(roks).mean()
@@ -604,6 +649,7 @@ def test_teacher_forced_headline_config_4096_envs():
     print(f"{label}: {frac:.4f} of {ok.size} sampled (env, step) "
           f"cases within tolerance ({hi:.4f} for the claimed envs >= {sim.grid}), rewards {rfrac:.4f}")
     err = _err_report(label, np.concatenate(eqs), np.concatenate(evs), ok.reshape(-1))
+    _hard_cap(np.concatenate(eqs), np.concatenate(evs), label)
     unexplained = _classify_misses(env_id, misses, sim.frame_skip)
     print(f"{label}: {len(misses)} misses, not explained by a discrete event: {unexplained}")
     _no_overflow(sim, n)

@@ -1,0 +1,254 @@
+"""Full-size GPU parity: the two capacity tiers and BASELINE's configurations at their real sizes.
+
+* Wide tier == fast tier: with every env-step forced through the wide-capacity tier
+  (aw_set_tier(1): MuJoCo's nconmax 100 / njmax 500, DAPG_assets.xml:4) the results are bitwise
+  those of the fast tier for every env-step that fits the fast capacities -- the wide tier is the
+  same code at larger capacities, so an env-step the fast tier hands over is finished exactly as
+  the fast tier would have finished it.
+* BASELINE config 3 (door / pen / relocate, 16 384 envs each, random policy) at its real size:
+  the persistent-claim launch (grid < n), 200 env-steps with auto-reset.  No env may drop a
+  constraint MuJoCo keeps (sticky AW_ST_*_OVERFLOW == 0: only MuJoCo's own caps can drop), and 256
+  envs sampled across the batch plus every env-step that went to the wide tier are teacher-forced
+  against the fp64 oracle (relocate_v0.py:85-93 resets, *_v0.py step).
+* The DAPG regime at the headline size (hammer-v0, 65 536 envs, the reference's pretrained
+  policy, mean actions as algos/baselines.py:82-86): 256 envs sampled across the batch are
+  teacher-forced through the hammer strike (hammer_v0.py:54-90).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ENVS, GOLDEN, make_oracle
+from test_gpu_parity import (ONE_STEP_MIN, REWARD_MIN, _classify_misses, _err_gate, _err_report, _hard_cap,
+                             _rewards_close, _state_err, f32)
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _t(a, dtype=None):
+    return torch.tensor(np.asarray(a), dtype=dtype or torch.float32, device="cuda")
+
+
+def _sim(env_id, n):
+    from mj_envs_amd import _native
+    from mj_envs_amd.tasks import attach_task, load_model
+    m = attach_task(load_model(env_id), env_id)
+    return m, _native.Sim(m.to_blob(), n)
+
+
+def _bufs(sim, n):
+    return (sim.empty(n, sim.obs_dim), sim.empty(n), sim.empty(n, dtype=torch.uint8),
+            sim.empty(n, dtype=torch.uint8))
+
+
+def _status(sim, n):
+    last, sticky = sim.empty(n, dtype=torch.int32), sim.empty(n, dtype=torch.int32)
+    sim.status(last, sticky)
+    torch.cuda.synchronize()
+    return last.cpu().numpy(), sticky.cpu().numpy()
+
+
+# --------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("env_id", ENVS)
+def test_wide_tier_bitwise_equals_fast_tier(env_id):
+    from mj_envs_amd import _native
+    n, steps = 512, 30
+    runs = []
+    for mode in (0, 1):
+        m, sim = _sim(env_id, n)
+        sim.set_tier(mode)
+        obs, rew, done, goal = _bufs(sim, n)
+        tobs = sim.empty(n, sim.obs_dim)
+        sim.reset(obs, seed=3)
+        ep = torch.from_numpy(np.arange(n, dtype=np.int32) % sim.horizon).cuda()
+        sim.set_episode(ep_len=ep)          # staggered: auto-resets (and their forwards) inside the run
+        act = sim.empty(n, sim.nu)
+        out = []
+        for k in range(steps):
+            sim.random_actions(act, 5, k)
+            sim.step(act, obs, rew, done, goal, terminal_obs=tobs, autoreset=True, seed=3)
+            out.append(torch.cat([obs, rew[:, None], done[:, None].float(), tobs], 1).clone())
+        q, v, w = sim.empty(n, sim.nq), sim.empty(n, sim.nv), sim.empty(n, sim.nv)
+        sim.get_state(q, v, w)
+        last, sticky = _status(sim, n)
+        runs.append((torch.stack(out), q, v, w, sticky))
+        if mode == 1:
+            assert ((sticky & _native.ST_WIDE) != 0).all(), "forced wide tier: every env must carry ST_WIDE"
+        else:
+            n_wide = int(((sticky & _native.ST_WIDE) != 0).sum())
+            print(f"{env_id}: automatic mode, {n_wide} of {n} envs took the wide tier at least once")
+        sim.close()
+    (a, qa, va, wa, sa), (b, qb, vb, wb, sb) = runs
+    assert torch.equal(a, b), f"{env_id}: obs / reward / done differ between the tiers"
+    assert torch.equal(qa, qb) and torch.equal(va, vb) and torch.equal(wa, wb)
+    assert ((sa & ~32) == (sb & ~32)).all()
+
+
+def test_wide_tier_reset_and_set_state_forward():
+    """aw_reset / aw_set_state through the wide tier: the same obs and state bit for bit"""
+    env_id, n = "relocate-v0", 256
+    outs = []
+    for mode in (0, 1):
+        m, sim = _sim(env_id, n)
+        sim.set_tier(mode)
+        obs, rew, done, goal = _bufs(sim, n)
+        sim.reset(obs, seed=4)
+        o1 = obs.clone()
+        act = sim.empty(n, sim.nu)
+        for k in range(20):
+            sim.random_actions(act, 2, k)
+            sim.step(act, obs, rew, done, goal)
+        q, v, w, p = sim.empty(n, sim.nq), sim.empty(n, sim.nv), sim.empty(n, sim.nv), sim.empty(n, sim.nparam)
+        sim.get_state(q, v, w, p)
+        o2 = sim.empty(n, sim.obs_dim)
+        sim.set_state(q, v, w, p, obs=o2)
+        torch.cuda.synchronize()
+        outs.append((o1, o2.clone(), q.clone()))
+        sim.close()
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+
+
+# --------------------------------------------------------------------------------------------
+C3_FULL_MIN = 0.995
+
+
+@pytest.mark.parametrize("env_id", ["door-v0", "pen-v0", "relocate-v0"])
+def test_config3_full_size_16384_envs(env_id):
+    """BASELINE configs[2] at its real size: 16 384 envs, grid < n (persistent claims), 200
+    env-steps with auto-reset from staggered phases.  Zero envs drop a constraint MuJoCo keeps;
+    teacher forcing on 256 sampled envs + every env-step the wide tier ran."""
+    from mj_envs_amd import _native
+    n, steps = 16384, 200
+    m, o = make_oracle(env_id)
+    _, sim = _sim(env_id, n)
+    assert sim.grid < n, f"grid {sim.grid} covers all {n} envs: the persistent claim path is not exercised"
+    assert (sim.maxcon, sim.maxefc) == (100, 500), "effective capacities must be MuJoCo's nconmax / njmax"
+    obs, rew, done, goal = _bufs(sim, n)
+    sim.reset(obs, seed=7)
+    sim.set_episode(ep_len=torch.from_numpy((np.arange(n) * 7919 % sim.horizon).astype(np.int32)).cuda())
+    sim.clear_status()
+    idx = np.unique(np.linspace(0, n - 1, 256).round().astype(int))
+    q, v, w, p = sim.empty(n, sim.nq), sim.empty(n, sim.nv), sim.empty(n, sim.nv), sim.empty(n, sim.nparam)
+    last = sim.empty(n, dtype=torch.int32)
+    act = sim.empty(n, sim.nu)
+    oks, roks, eqs, evs, misses = [], [], [], [], []
+    wide_cases, wide_ok = 0, 0
+    for k in range(steps):
+        sim.get_state(q, v, w, p)
+        torch.cuda.synchronize()
+        pre = dict(qpos=q.cpu().numpy().astype(np.float64), qvel=v.cpu().numpy().astype(np.float64),
+                   warm=w.cpu().numpy().astype(np.float64), params=p.cpu().numpy().astype(np.float64))
+        sim.random_actions(act, 9, k)
+        sim.step(act, obs, rew, done, goal, autoreset=True, seed=7)
+        sim.get_state(q, v)
+        sim.status(last)
+        torch.cuda.synchronize()
+        dn = done.cpu().numpy()
+        lw = (last.cpu().numpy() & _native.ST_WIDE) != 0
+        # the envs compared this step: the sample and every wide-tier env-step, minus the envs whose
+        # episode ended (auto-reset: the post-step state is the new episode's)
+        sel = np.union1d(idx, np.nonzero(lw)[0])
+        sel = sel[dn[sel] == 0]
+        a = act.cpu().numpy().astype(np.float64)
+        st = {key: val[sel].copy() for key, val in pre.items()}
+        _, r_ref, _, _, ost = o.step(st, a[sel], nthreads=8)
+        assert not (np.bitwise_or.reduce(ost) & 24), "oracle dropped constraints at MuJoCo's caps"
+        qg, vg = q.cpu().numpy()[sel], v.cpu().numpy()[sel]
+        eq, ev, okk = _state_err(qg, vg, st["qpos"], st["qvel"])
+        oks.append(okk)
+        eqs.append(eq)
+        evs.append(ev)
+        wide_cases += int(lw[sel].sum())
+        wide_ok += int(okk[lw[sel]].sum())
+        misses += [(k, int(sel[j]), pre["params"][sel[j]], pre["qpos"][sel[j]], pre["qvel"][sel[j]], pre["warm"][sel[j]],
+                    a[sel[j]], qg[j].astype(np.float64), vg[j].astype(np.float64)) for j in np.where(~okk)[0]]
+        roks.append(_rewards_close(rew.cpu().numpy()[sel], r_ref, check=False))
+    _, sticky = _status(sim, n)
+    n_over = int(((sticky & _native.ST_OVERFLOW) != 0).sum())
+    n_wide = int(((sticky & _native.ST_WIDE) != 0).sum())
+    ok = np.concatenate(oks)
+    frac, rfrac = ok.mean(), np.concatenate(roks).mean()
+    label = f"config 3 {env_id} ({n} envs, grid {sim.grid}, {steps} steps)"
+    print(f"{label}: {frac:.4f} of {ok.size} teacher-forced (env, step) cases within tolerance, rewards {rfrac:.4f}; "
+          f"{n_wide} envs took the wide tier ({wide_cases} compared env-steps, {wide_ok} within tolerance); "
+          f"envs dropping constraints at MuJoCo's caps: {n_over}")
+    err = _err_report(label, np.concatenate(eqs), np.concatenate(evs), ok)
+    _hard_cap(np.concatenate(eqs), np.concatenate(evs), label)
+    unexplained = _classify_misses(env_id, misses, sim.frame_skip)
+    print(f"{label}: {len(misses)} misses, unexplained: {unexplained}")
+    assert n_over == 0, f"{n_over} envs dropped constraints"
+    assert frac >= C3_FULL_MIN and rfrac >= REWARD_MIN, (frac, rfrac)
+    assert not unexplained, unexplained
+    _err_gate(err)
+
+
+# --------------------------------------------------------------------------------------------
+DAPG_HEADLINE_MIN = 0.998
+
+
+def test_dapg_teacher_forced_headline_size():
+    """hammer-v0, 65 536 envs in the DAPG closed loop (k_mlp mean actions): 256 envs sampled across
+    the batch teacher-forced over env-steps 40..119 (grasp, lift, the strike on the nail)."""
+    from mj_envs_amd import _native
+    from mj_envs_amd.policy import GaussianMLP
+    env_id, n, warm_steps, steps = "hammer-v0", 65536, 40, 80
+    m, o = make_oracle(env_id)
+    _, sim = _sim(env_id, n)
+    assert sim.grid < n
+    pol = GaussianMLP.from_npz(os.path.join(GOLDEN, "dapg_hammer.npz"), device=0)
+    obs, rew, done, goal = _bufs(sim, n)
+    act = sim.empty(n, sim.nu)
+    sim.reset(obs, seed=31)
+    for k in range(warm_steps):
+        pol.act(obs, out=act)
+        sim.step(act, obs, rew, done, goal)
+    idx = np.unique(np.linspace(0, n - 1, 256).round().astype(int))
+    q, v, w, p = sim.empty(n, sim.nq), sim.empty(n, sim.nv), sim.empty(n, sim.nv), sim.empty(n, sim.nparam)
+    oks, roks, eqs, evs, misses = [], [], [], [], []
+    sim.get_state(params=p)
+    torch.cuda.synchronize()
+    P = p.cpu().numpy().astype(np.float64)[idx]
+    for k in range(steps):
+        sim.get_state(q, v, w)
+        pol.act(obs, out=act)
+        torch.cuda.synchronize()
+        st = dict(qpos=q.cpu().numpy()[idx].astype(np.float64), qvel=v.cpu().numpy()[idx].astype(np.float64),
+                  warm=w.cpu().numpy()[idx].astype(np.float64), params=P.copy())
+        pre = {key: val.copy() for key, val in st.items()}
+        a = act.cpu().numpy()[idx].astype(np.float64)
+        sim.step(act, obs, rew, done, goal)
+        sim.get_state(q, v)
+        torch.cuda.synchronize()
+        _, r_ref, _, _, _ = o.step(st, a, nthreads=8)
+        qg, vg = q.cpu().numpy()[idx], v.cpu().numpy()[idx]
+        eq, ev, okk = _state_err(qg, vg, st["qpos"], st["qvel"])
+        oks.append(okk)
+        eqs.append(eq)
+        evs.append(ev)
+        misses += [(warm_steps + k, int(idx[j]), pre["params"][j], pre["qpos"][j], pre["qvel"][j], pre["warm"][j],
+                    a[j], qg[j].astype(np.float64), vg[j].astype(np.float64)) for j in np.where(~okk)[0]]
+        roks.append(_rewards_close(rew.cpu().numpy()[idx], r_ref, check=False))
+    ok = np.concatenate(oks)
+    frac, rfrac = ok.mean(), np.concatenate(roks).mean()
+    label = f"DAPG headline size (hammer-v0, {n} envs, grid {sim.grid})"
+    print(f"{label}: {frac:.4f} of {ok.size} sampled (env, step) cases within tolerance, rewards {rfrac:.4f}")
+    err = _err_report(label, np.concatenate(eqs), np.concatenate(evs), ok)
+    _hard_cap(np.concatenate(eqs), np.concatenate(evs), label)
+    unexplained = _classify_misses(env_id, misses, sim.frame_skip)
+    print(f"{label}: {len(misses)} misses at steps {sorted(set(ms[0] for ms in misses))}, unexplained: {unexplained}")
+    _, sticky = _status(sim, n)
+    assert not ((sticky & _native.ST_OVERFLOW) != 0).any()
+    assert frac >= ONE_STEP_MIN and rfrac >= REWARD_MIN, (frac, rfrac)
+    assert not unexplained, unexplained
+    _err_gate(err)
+    print(f"{label}: DAPG_HEADLINE_MIN target {DAPG_HEADLINE_MIN}: {'met' if frac >= DAPG_HEADLINE_MIN else 'NOT met'}")
