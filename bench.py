@@ -322,11 +322,14 @@ def main():
         if int(os.environ["WORLD_SIZE"]) != args.gpus:
             raise SystemExit(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}")
     elif args.gpus > 1 or args.launch or args.dry_run:
-        # parent: count devices (no HIP context is created by device_count on this image) and start
-        # one child per GPU; this process never initialises the GPU and never execs
+        # parent: count devices without any HIP call (AMD SMI / the KFD topology, dist.count_gpus)
+        # and start one child per GPU; this process never initialises the GPU and never execs
         if not args.dry_run:
-            import torch
-            have = torch.cuda.device_count()
+            from mj_envs_amd.dist import count_gpus
+            try:
+                have = count_gpus()
+            except RuntimeError as e:
+                raise SystemExit(f"bench.py --gpus {args.gpus}: cannot count GPUs ({e}); refusing to run")
             if have < args.gpus:
                 raise SystemExit(f"bench.py --gpus {args.gpus}: only {have} GPU(s) visible; refusing to run "
                                  f"on fewer ranks")
@@ -456,8 +459,8 @@ def main():
     if rank == 0:
         total_steps = world * n * args.steps
         value = total_steps / elapsed
-        flops, counts = perfmodel.step_flops(env_id, m, sim.frame_skip)
-        flops_dense, _ = perfmodel.step_flops(env_id, m, sim.frame_skip, dense_m=True)
+        flops, counts = perfmodel.step_flops(env_id, m, sim.frame_skip, policy=args.policy)
+        flops_dense, _ = perfmodel.step_flops(env_id, m, sim.frame_skip, dense_m=True, policy=args.policy)
         achieved = flops * n / (kern_ms * 1e-3) / 1e12
         bytes_step = perfmodel.step_bytes(sim.nq, sim.nv, sim.nu, sim.obs_dim, sim.nparam)
         build_id = _native.kernel_build_id()
@@ -470,6 +473,7 @@ def main():
                     kernel=f"k_step<{sim.task_kind}>", nv=sim.nv, kernel_ms=round(kern_ms, 4),
                     kernel_ms_min_max=[round(min(kern), 4), round(max(kern), 4)],
                     flops_per_env_step=round(flops), bytes_per_env_step=bytes_step,
+                    work_counts=dict(source=counts["source"], policy=counts["policy"], avg=counts["avg"]),
                     flops_formula="MuJoCo 2.1's algorithms: tree-sparse mj_factorM / mj_solveM for M, dense "
                                   "Cholesky only for the Newton Hessian (perfmodel.py)",
                     r03_dense_formula=dict(flops_per_env_step=round(flops_dense),
@@ -486,7 +490,7 @@ def main():
                     traffic_raw_over_algorithmic=round(traffic_raw / n / bytes_step, 3) if traffic_raw else None,
                     note="FP32 roofline (157.3 TFLOP/s: the vector peak, equal to the fp32 MFMA peak the contact Hessian J'DJ, "
                          "the CRB mass-matrix product and the noslip pair coupling run on); FLOPs "
-                         "from perfmodel.py on profiles/work_counts_hammer.json. The HBM figures are far from "
+                         "from perfmodel.py on the oracle's work counts of this regime (work_counts). The HBM figures are far from "
                          "8 TB/s by construction: ~1.1 KB compulsory traffic per env-step (SURVEY 8d), the "
                          "north-star's 40 % of HBM roofline is unreachable on algorithmic bytes")
         workload = (f"{env_id}, {n} envs per GPU (north-star config), random policy, staggered episode phases "

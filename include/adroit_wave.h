@@ -164,7 +164,7 @@ int aw_task_eval(aw_handle* h, int n, const float* qpos, const float* qvel, cons
 /* Introspection for parity tests: run mj_forward (no integration) on env `env` of the
  * current state with raw control `ctrl` [nu] (NULL = 0) and copy internals into out (fp32,
  * AW_DUMP_SIZE floats; layout: mj_envs_amd/_native.py DUMP_LAYOUT). */
-#define AW_DUMP_SIZE 3208
+#define AW_DUMP_SIZE 3400
 int aw_forward_dump(aw_handle* h, int env, const float* ctrl, float* out, void* stream);
 
 /* Depth camera observation (the reference renders RGB through OpenGL:
@@ -194,10 +194,12 @@ int aw_policy_mlp(int n, int in_dim, int hidden, int out_dim, const float* param
  * mat [n][2][9] (row-major rotations), size [n][2][3], margin [n] -> count [n] and out
  * [n][AW_MAXPAIRCON][7] = (dist, pos[3], normal[3]) in emission order, the normal pointing from
  * the lower-type geom to the other (MuJoCo's geom1 -> geom2).  The MPR collider runs at the
- * handle's precision.  Used by the exact-geometry collider tests against the oracle. */
+ * handle's precision.  out64 (may be NULL): [n][AW_MAXPAIRCON][7] fp64, the MPR (cylinder) pairs'
+ * contacts before rounding to fp32.  Used by the exact-geometry collider tests against the oracle. */
 #define AW_MAXPAIRCON 8
 int aw_collide_test(aw_handle* h, int n, const int32_t* types, const float* pos, const float* mat,
-                    const float* size, const float* margin, float* out, int32_t* count, void* stream);
+                    const float* size, const float* margin, float* out, int32_t* count, double* out64,
+                    void* stream);
 
 /* Diagnostic: per-stage shader-clock cycles of k_step summed over all waves since the last
  * reset (40 counters, see aw_common.h PR_*).  Only libraries built with -DAW_STAGE_PROF

@@ -34,13 +34,13 @@ def dump_layout(maxcon=MAXCON, maxefc=MAXEFC):
                 scalars=(1760, 8), con_dist=(c, maxcon), con_pos=(c + maxcon, 3 * maxcon),
                 con_frame=(c + 4 * maxcon, 9 * maxcon), con_pair=(c + 13 * maxcon, maxcon),
                 efc_force=(e, maxefc), efc_aref=(e + maxefc, maxefc), efc_D=(e + 2 * maxefc, maxefc),
-                efc_type=(e + 3 * maxefc, maxefc))
+                efc_type=(e + 3 * maxefc, maxefc), efc_state=(e + 4 * maxefc, maxefc))
 
 
 DUMP_LAYOUT = dump_layout()
 # why the Newton solve stopped (aw_solver.h NT_EXIT_*)
 NT_EXIT = ("max_iterations", "no_descent", "fp32_noise_floor", "improvement", "gradient", "no_constraints")
-AW_DUMP_SIZE = 1768 + 14 * MAXCON + 4 * MAXEFC
+AW_DUMP_SIZE = 1768 + 14 * MAXCON + 5 * MAXEFC
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -79,7 +79,7 @@ def load():
     L.aw_task_eval.argtypes = [_vp, ctypes.c_int] + [_vp] * 10 + [_vp]
     L.aw_forward_dump.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp]
     L.aw_stage_profile.argtypes = [_vp, ctypes.c_int]
-    L.aw_collide_test.argtypes = [_vp, ctypes.c_int] + [_vp] * 8
+    L.aw_collide_test.argtypes = [_vp, ctypes.c_int] + [_vp] * 9
     L.aw_collide_test.restype = ctypes.c_int
     # (diagnostic builds of older revisions, selected with AW_LIB, may lack the newer entry points;
     # calling one of those then raises AttributeError)
@@ -279,17 +279,21 @@ class Sim:
         assert c.size == 17, "render_depth: camera record has 17 floats"
         _check(load().aw_render_depth(self.h, c.ctypes.data, w, h, _ptr(out), _stream()))
 
-    def collide_test(self, types, pos, mat, size, margin):
-        """narrowphase of n primitive pairs (test hook): list of arrays [(dist, pos[3], normal[3]), ...]"""
+    def collide_test(self, types, pos, mat, size, margin, fp64: bool = False):
+        """narrowphase of n primitive pairs (test hook): list of arrays [(dist, pos[3], normal[3]), ...]
+        (fp64: the MPR pairs' fp64 results instead of the fp32 contacts)"""
         import torch
         n = len(types)
         dev = self.torch_device
         t = lambda a, dt=torch.float32: torch.tensor(np.asarray(a), dtype=dt, device=dev).contiguous()
         out = torch.zeros(n, 8, 7, device=dev)
         cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+        out64 = torch.zeros(n, 8, 7, dtype=torch.float64, device=dev) if fp64 else None
         args = [t(types, torch.int32), t(pos), t(mat), t(size), t(margin)]   # alive until the kernel ran
-        _check(load().aw_collide_test(self.h, n, *[_ptr(a) for a in args], _ptr(out), _ptr(cnt), _stream()))
-        o, c = out.cpu().numpy().astype(np.float64), cnt.cpu().numpy()
+        _check(load().aw_collide_test(self.h, n, *[_ptr(a) for a in args], _ptr(out), _ptr(cnt), _ptr(out64),
+                                      _stream()))
+        o = (out64 if fp64 else out).cpu().numpy().astype(np.float64)
+        c = cnt.cpu().numpy()
         return [o[i, :c[i]] for i in range(n)]
 
     def forward_dump(self, env: int, ctrl=None) -> dict:
@@ -313,6 +317,6 @@ class Sim:
         res["con_pos"] = res["con_pos"][:3 * ncon].reshape(ncon, 3)
         res["con_frame"] = res["con_frame"][:9 * ncon].reshape(ncon, 9)
         res["con_pair"] = res["con_pair"][:ncon].astype(int)
-        for k in ("efc_force", "efc_aref", "efc_D", "efc_type"):
+        for k in ("efc_force", "efc_aref", "efc_D", "efc_type", "efc_state"):
             res[k] = res[k][:nefc]
         return res

@@ -256,8 +256,9 @@ struct Dof {
 // mj_forward: everything up to qacc / forces / sensors; Mrow is left in registers.  Stage order
 // follows the LDS overlays (aw_common.h Env): the constraint rows are assembled while the
 // phase-K arrays (cdof, subcom) are alive, then the solver phase reuses that storage.
-template <int TASK, bool KEEP_D = false>
-AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[Tree<TASK>::NV], Dof& d) {
+// ROWST (aw_forward_dump only): the Newton solve's final row states (S_*) go to rowst[r]
+template <int TASK, bool ROWST = false>
+AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[Tree<TASK>::NV], Dof& d, float* rowst = nullptr) {
   constexpr int NV = Tree<TASK>::NV;
   stage_kinematics(m, s, lane);
   AW_PROF(s, PR_KIN);
@@ -287,9 +288,9 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[Tree<TASK>:
     d.qfrc_con = 0.f;
   } else {
     float a = 0.f;
-    solve_newton<NV>(m, s, lane, Mrow, a, d.qfrc_smooth, d.qacc_smooth);
+    solve_newton<NV, ROWST>(m, s, lane, Mrow, a, d.qfrc_smooth, d.qacc_smooth, rowst);
     AW_PROF(s, PR_NEWTON);
-    if (m.noslip_iterations > 0 && !(m.disableflags & DSBL_NOSLIP)) solve_noslip<TASK, KEEP_D>(m, s, lane, Mrow, a);
+    if (m.noslip_iterations > 0 && !(m.disableflags & DSBL_NOSLIP)) solve_noslip<TASK>(m, s, lane, Mrow, a);
     AW_PROF(s, PR_NOSLIP);
     for (int r = lane; r < s.nefc; r += 64) s.rowbuf[r] = s.efc_force[r];
     wsync();
@@ -731,7 +732,7 @@ __global__ void __launch_bounds__(64) k_step_wide(const DModel* __restrict__ mpt
 #ifndef AW_WIDE   // introspection: fast tier only
 // dump layout (floats): see mj_envs_amd/_native.py dump_layout (same offsets from the capacities)
 constexpr int DUMP_SCAL = 1760, DUMP_CON = 1768, DUMP_EFC = DUMP_CON + 14 * MAXCON;
-static_assert(DUMP_EFC + 4 * MAXEFC == AW_DUMP_SIZE, "AW_DUMP_SIZE out of date");
+static_assert(DUMP_EFC + 5 * MAXEFC == AW_DUMP_SIZE, "AW_DUMP_SIZE out of date");
 template <int TASK>
 __global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const float* ctrl, float* out) {
   constexpr int NV = Tree<TASK>::NV;
@@ -742,7 +743,8 @@ __global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const
   stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
   float Mrow[NV];
   Dof d;
-  forward<TASK, true>(m, s, lane, Mrow, d);   // efc_D kept out of noslip's parking
+  for (int r = lane; r < MAXEFC; r += 64) out[DUMP_EFC + 4 * MAXEFC + r] = -1.f;
+  forward<TASK, true>(m, s, lane, Mrow, d, out + DUMP_EFC + 4 * MAXEFC);   // + the Newton row states
   for (int i = lane; i < MAXB * 3; i += 64) out[i] = i < m.nbody * 3 ? (&s.xpos[0][0])[i] : 0.f;
   for (int i = lane; i < MAXB * 4; i += 64) out[96 + i] = i < m.nbody * 4 ? (&s.xquat[0][0])[i] : 0.f;
   for (int i = lane; i < MAXS * 3; i += 64) out[224 + i] = i < m.nsite * 3 ? (&s.sxpos[0][0])[i] : 0.f;
@@ -846,7 +848,7 @@ AW_DEV void collide_gv(const DModel& m, const GV& a, const GV& b, float margin, 
 
 __global__ void __launch_bounds__(64) k_collide_test(DModel m, int n, const int* types, const float* pos,
                                                      const float* mat, const float* size, const float* margin,
-                                                     float* out, int* count) {
+                                                     float* out, int* count, double* out64) {
   __shared__ Env s;
   const int i = blockIdx.x, lane = threadIdx.x;
   if (i >= n) return;
@@ -860,7 +862,7 @@ __global__ void __launch_bounds__(64) k_collide_test(DModel m, int n, const int*
       for (int k = 0; k < 9; k++) g[q].mat[k] = mat[18 * i + 9 * q + k];
     }
     const int f = g[0].type <= g[1].type ? 0 : 1;
-    Emit e{&s, 0, 0};
+    Emit e{&s, 0, 0, out64 ? out64 + (size_t)i * MAXPAIRCON * 7 : nullptr};
     collide_gv(m, g[f], g[1 - f], margin[i], e, lane);
   }
   wsync();
@@ -1763,12 +1765,12 @@ int aw_policy_mlp(int n, int in_dim, int hidden, int out_dim, const float* param
 }
 
 int aw_collide_test(aw_handle* h, int n, const int32_t* types, const float* pos, const float* mat, const float* size,
-                    const float* margin, float* out, int32_t* count, void* stream) {
+                    const float* margin, float* out, int32_t* count, double* out64, void* stream) {
   if (!h || n <= 0 || !types || !pos || !mat || !size || !margin || !out || !count)
     return fail(AW_EINVAL, "aw_collide_test: bad arguments");
   HIPCHK(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_collide_test, dim3(n), dim3(64), 0, st, h->m, n, types, pos, mat, size, margin, out, count);
+  hipLaunchKernelGGL(k_collide_test, dim3(n), dim3(64), 0, st, h->m, n, types, pos, mat, size, margin, out, count, out64);
   HIPCHK(hipGetLastError());
   return AW_OK;
 }

@@ -24,6 +24,7 @@ struct Emit {
   Env* s;
   int pair;
   int cnt;
+  double* out64 = nullptr;   // test hook (aw_collide_test): the MPR's fp64 (dist, pos, normal) per contact
 };
 
 AW_DEV void axis_of(float* a, const float* m, int k) { a[0] = m[k]; a[1] = m[3 + k]; a[2] = m[6 + k]; }
@@ -559,12 +560,45 @@ namespace mpr {
 // point on line / face contacts (a cylinder lying on a box) moves between the ends of the line
 // under 1e-7 rad of rotation, i.e. under fp32 kinematics.  (An fp32 path with fp32 inputs measured
 // 81 % teacher-forced parity on pen and 99.4 % on hammer's C3 run; it was removed in round 3.)
+//
+// Operation order: libccd's, as the oracle states it (oracle/collide.cc namespace mpr) -- every
+// product and sum rounded separately (no fused multiply-add: the pragma below holds for the MPR
+// code and its local vector helpers), normalisation as 1 / sqrt(|v|^2) with the correctly rounded
+// fp64 sqrt and divide, the cylinder's radial support as ld / |ld_xy| * r.  On identical inputs the
+// kernel's portal, depth, normal and point are then bitwise the oracle's -- including the line /
+// face contacts (a cylinder lying on a box), whose point is ill-conditioned along the line
+// (tests/test_colliders.py test_gpu_mpr_pairs_match_oracle).
+#ifndef AW_MPR_FAST
+#pragma clang fp contract(off)
+#endif
 // libccd's CCD_EPS of the matching build: DBL_EPSILON (MuJoCo's double build) / FLT_EPSILON
 template <class T> constexpr T EPS_T = sizeof(T) == 8 ? T(2.220446049250313e-16) : T(1.1920928955078125e-07);
 template <class T> struct GVdT {
   T pos[3], mat[9], size[3];
   int type;
 };
+// local vector helpers (compiled under the pragma above: no contraction)
+template <class T> AW_DEV T dot3(const T* a, const T* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+template <class T> AW_DEV void cross3(T* r, const T* a, const T* b) {
+  T t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+template <class T> AW_DEV void sub3(T* r, const T* a, const T* b) { r[0] = a[0] - b[0]; r[1] = a[1] - b[1]; r[2] = a[2] - b[2]; }
+template <class T> AW_DEV void add3(T* r, const T* a, const T* b) { r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2]; }
+template <class T> AW_DEV void scl3(T* r, const T* a, T s) { r[0] = a[0] * s; r[1] = a[1] * s; r[2] = a[2] * s; }
+template <class T> AW_DEV void copy3(T* r, const T* a) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; }
+template <class T> AW_DEV void mulmv3(T* r, const T* m, const T* v) {
+  T t0 = m[0] * v[0] + m[1] * v[1] + m[2] * v[2];
+  T t1 = m[3] * v[0] + m[4] * v[1] + m[5] * v[2];
+  T t2 = m[6] * v[0] + m[7] * v[1] + m[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+template <class T> AW_DEV void mulmtv3(T* r, const T* m, const T* v) {
+  T t0 = m[0] * v[0] + m[3] * v[1] + m[6] * v[2];
+  T t1 = m[1] * v[0] + m[4] * v[1] + m[7] * v[2];
+  T t2 = m[2] * v[0] + m[5] * v[1] + m[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
 template <class T> AW_DEV bool is_zero(T x) { return fabs(x) < EPS_T<T>; }
 template <class T> AW_DEV bool eq(T a, T b) {
   T ab = fabs(a - b);
@@ -574,7 +608,11 @@ template <class T> AW_DEV bool eq(T a, T b) {
 }
 template <class T> AW_DEV bool veq(const T* a, const T* b) { return eq(a[0], b[0]) && eq(a[1], b[1]) && eq(a[2], b[2]); }
 template <class T> AW_DEV void vnorm(T* v) {
+#ifdef AW_MPR_FAST
   T k = rsqrt_fast(dot3(v, v));
+#else
+  T k = T(1.0) / sqrt(dot3(v, v));   // ccdVec3Normalize
+#endif
   scl3(v, v, k);
 }
 template <class T> AW_DEV T sgn(T x) { return x < 0 ? -T(1.0) : (x > 0 ? T(1.0) : T(0.0)); }
@@ -591,11 +629,21 @@ template <class T> AW_DEV void gsupport(T* res, const GVdT<T>& g, const T* dir, 
   const bool box = g.type == GEOM_BOX, cyl = g.type == GEOM_CYLINDER, cap = g.type == GEOM_CAPSULE;
   const bool round = g.type == GEOM_SPHERE || cap;
   const T sg0 = sgn(ld[0]), sg1 = sgn(ld[1]), sg2 = sgn(ld[2]);
+#ifdef AW_MPR_FAST
   const T t2 = ld[0] * ld[0] + ld[1] * ld[1];   // the cylinder's radial direction: |ld_xy| > MINVAL
   const T ci = t2 > T(MINVAL) * T(MINVAL) ? s[0] * rsqrt_fast(t2) : T(0.0);
-  r[0] = box ? sg0 * s[0] : (cyl ? ld[0] * ci : (round ? ld[0] * s[0] : T(0.0)));
-  r[1] = box ? sg1 * s[1] : (cyl ? ld[1] * ci : (round ? ld[1] * s[0] : T(0.0)));
-  r[2] = box ? sg2 * s[2] : (cyl ? sg2 * s[1] : (round ? fma(ld[2], s[0], cap ? sg2 * s[1] : T(0.0)) : T(0.0)));
+  const T cx = ld[0] * ci, cy = ld[1] * ci;
+  const T rz = fma(ld[2], s[0], cap ? sg2 * s[1] : T(0.0));
+#else
+  // the oracle's (mjccd_support's) order: cylinder ld / |ld_xy| * r, capsule ld r + sign h
+  const T tmp = sqrt(ld[0] * ld[0] + ld[1] * ld[1]);
+  const bool rad = tmp > T(MINVAL);
+  const T cx = rad ? ld[0] / tmp * s[0] : T(0.0), cy = rad ? ld[1] / tmp * s[0] : T(0.0);
+  const T rz = ld[2] * s[0] + (cap ? sg2 * s[1] : T(0.0));
+#endif
+  r[0] = box ? sg0 * s[0] : (cyl ? cx : (round ? ld[0] * s[0] : T(0.0)));
+  r[1] = box ? sg1 * s[1] : (cyl ? cy : (round ? ld[1] * s[0] : T(0.0)));
+  r[2] = box ? sg2 * s[2] : (cyl ? sg2 * s[1] : (round ? rz : T(0.0)));
   for (int k = 0; k < 3; k++) r[k] += ld[k] * margin / 2;
   mulmv3(res, g.mat, r);
   add3(res, res, g.pos);
@@ -674,7 +722,7 @@ template <class T> AW_DEV int discover(const Ctx<T>& c, PortalT<T>& P) {
   sub3(P.p0.v, P.p0.v1, P.p0.v2);
   const T zero[3] = {0, 0, 0};
   if (veq(P.p0.v, zero)) P.p0.v[0] += EPS_T<T> * 10;
-  scl3(dir, P.p0.v, -1);
+  scl3(dir, P.p0.v, T(-1));
   vnorm(dir);
   support(c, dir, P.p1);
   T d = dot3(P.p1.v, dir);
@@ -695,7 +743,7 @@ template <class T> AW_DEV int discover(const Ctx<T>& c, PortalT<T>& P) {
     setsup(t, P.p1);
     selsup(P.p1, sw, P.p2);
     selsup(P.p2, sw, t);
-    if (sw) scl3(dir, dir, -1);
+    if (sw) scl3(dir, dir, T(-1));
   }
   for (int it = 0; it < 1000; it++) {
     support(c, dir, P.p3);
@@ -832,6 +880,9 @@ template <class T> AW_DEV int penetration(const Ctx<T>& c, T* depth, T* dir, T* 
     expand(P, v4);
   }
 }
+#ifndef AW_MPR_FAST
+#pragma clang fp contract(fast)
+#endif
 }  // namespace mpr
 
 // fp64 pose of collidable geom g from the fp64 body frames (stage_kin64), as the oracle's
@@ -863,6 +914,11 @@ AW_DEV void c_convex64(const DModel& m, const mpr::GVdT<double>& own, int half, 
   const float pf[3] = {(float)pos[0], (float)pos[1], (float)pos[2]};
   const float df[3] = {(float)dir[0], (float)dir[1], (float)dir[2]};
   if (half) return;
+  if (e.out64 && e.cnt < MAXPAIRCON) {
+    double* o = e.out64 + 7 * e.cnt;
+    o[0] = dist;
+    for (int k = 0; k < 3; k++) { o[1 + k] = pos[k]; o[4 + k] = dir[k]; }
+  }
   emit(e, (float)dist, pf, df);
 }
 

@@ -574,9 +574,9 @@ AW_DEV void hess_dense_mfma(const DModel& m, Env& s, int lane) {
   }
 }
 
-template <int NV>
+template <int NV, bool ROWST = false>
 AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mrow)[NV], float& a, float qfrc_smooth,
-                         float qacc_smooth) {
+                         float qacc_smooth, float* rowst = nullptr) {
   const int lane = lane_nt;
   const int nefc = s.nefc;
   const float fs = lane < NV ? qfrc_smooth : 0.f;
@@ -845,6 +845,7 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
   for (int h = 0; h < NRL; h++) {
     int r = lane + 64 * h;
     if (r < nefc) s.efc_force[r] = rr[h].force;
+    if (ROWST && r < nefc) rowst[r] = (float)rr[h].st;
   }
   wsync();
 }
@@ -865,7 +866,7 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
 // lo = -lim - fa, hi = lim + fb (dof rows: fa = f, fb = -f, lim = frictionloss; pairs: fa = f1,
 // fb = f2, lim = 0), and the row's cost change is diag d (d / 2 - y).  Pairs past the lanes
 // (npr > npl, rare) rebuild their column of A every sweep.
-template <int TASK, bool KEEP_D>
+template <int TASK>
 AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mrow)[Tree<TASK>::NV], float& qacc) {
   const int lane = lane_ns;
   constexpr int NV = Tree<TASK>::NV;

@@ -119,6 +119,48 @@ class EpisodeTotals:
                     success_pct=100.0 * int(s.sum()) / max(n, 1))
 
 
+def _visible(n_phys: int) -> int:
+    """devices left by the HIP / ROCr / CUDA visibility lists (the runtime applies them in turn)"""
+    n = n_phys
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is None:
+            continue
+        ids = [x for x in v.split(",") if x.strip() != ""]
+        n = min(n, len(ids))
+    return n
+
+
+def count_gpus() -> int:
+    """GPUs this process may use, counted WITHOUT a HIP call (the launcher parent must never
+    initialise the GPU it hands to its child ranks): AMD SMI's processor handles, else the KFD
+    topology (nodes with SIMDs), then the visibility variables.  Raises RuntimeError when neither
+    source answers -- never falls back to the HIP runtime."""
+    n = None
+    try:
+        import amdsmi
+        amdsmi.amdsmi_init()
+        try:
+            n = len(amdsmi.amdsmi_get_processor_handles())
+        finally:
+            amdsmi.amdsmi_shut_down()
+    except Exception:
+        n = None
+    if n is None:
+        root = "/sys/class/kfd/kfd/topology/nodes"
+        try:
+            n = 0
+            for d in os.listdir(root):
+                with open(os.path.join(root, d, "properties")) as f:
+                    props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+                n += int(props.get("simd_count", "0")) > 0
+        except OSError:
+            n = None
+    if n is None:
+        raise RuntimeError("count_gpus: neither AMD SMI nor the KFD topology is available")
+    return _visible(n)
+
+
 def free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

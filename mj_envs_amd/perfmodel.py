@@ -3,8 +3,10 @@
 The step kernel is neither HBM- nor MFMA-bound: its state stays on chip for all substeps.
 Its roofline is the FP32 compute rate (157.3 TFLOP/s on gfx950, shared by VALU and the
 f32-input MFMA), priced with the formula below on the average per-substep counts (contacts,
-constraint rows, Newton / noslip iterations) logged by the CPU oracle on a hammer-v0 random-
-policy trajectory (profiles/work_counts_hammer.json, made by tools/work_counts.py).
+constraint rows, Newton iterations, line-search evaluations per Newton iteration, noslip sweeps)
+logged by the CPU oracle in the regime the bench times: random actions
+(profiles/work_counts_<task>.json) or the pretrained DAPG closed loop (work_counts_<task>_dapg.json),
+both made by tools/work_counts.py.
 
 One FLOP = one fp32 add or multiply (an FMA counts 2).  The formula counts the arithmetic
 MuJoCo 2.1's own algorithms do: the joint-space inertia M is factored and
@@ -114,12 +116,19 @@ def model_dims(model) -> dict:
                 factor_m=tree_factor_flops(model.dof_parentid), solve_m=tree_solve_flops(model.dof_parentid))
 
 
-def counts_path(env_id: str) -> str:
+def counts_path(env_id: str, policy: str = "none") -> str:
+    """the oracle's work counts of the regime the bench times: the DAPG closed loop
+    (work_counts_<task>_dapg.json) or i.i.d. random actions (work_counts_<task>.json)"""
     here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    return os.path.join(here, "profiles", f"work_counts_{env_id.split('-')[0]}.json")
+    suffix = "_dapg" if policy == "dapg" else ""
+    return os.path.join(here, "profiles", f"work_counts_{env_id.split('-')[0]}{suffix}.json")
 
 
-def step_flops(env_id: str, model, frame_skip: int, dense_m: bool = False) -> tuple[float, dict]:
-    with open(counts_path(env_id)) as f:
+def step_flops(env_id: str, model, frame_skip: int, dense_m: bool = False, policy: str = "none") -> tuple[float, dict]:
+    """FLOPs per env-step priced on the oracle-logged counts of the same regime (policy "dapg":
+    the pretrained DAPG closed loop; otherwise the random-action counts)"""
+    path = counts_path(env_id, policy)
+    with open(path) as f:
         c = json.load(f)
+    c["source"] = os.path.relpath(path, os.path.dirname(os.path.dirname(path)))
     return frame_skip * substep_flops(model_dims(model), c["avg"], dense_m=dense_m), c

@@ -134,8 +134,9 @@ int or_step(void* p, int n, const double* params, const double* action, double* 
 }
 
 /* or_step + per-env work counts of the env-step (test / profiling hook, tools/work_counts.py):
- * stats[e][8] = max ncon, max nefc, max dense (contact) rows over the frame_skip substeps, summed
- * Newton iterations, line-search derivative evaluations and noslip sweeps, substeps, status */
+ * stats[e][12] = max ncon, max nefc, max dense (contact) rows over the frame_skip substeps, summed
+ * Newton iterations, line-search derivative evaluations and noslip sweeps, substeps, status, summed
+ * ncon, nefc and dense rows, 0 */
 int or_step_stats(void* p, int n, const double* params, const double* action, double* qpos, double* qvel,
                   double* warm, double* obs, double* reward, uint8_t* done, uint8_t* goal, int32_t* stats,
                   int nthreads) {
@@ -160,8 +161,8 @@ int or_step_stats(void* p, int n, const double* params, const double* action, do
         double x = a[i] < -1.0 ? -1.0 : (a[i] > 1.0 ? 1.0 : a[i]);
         d.ctrl[i] = m->task_act_mid[i] + x * m->task_act_rng[i];
       }
-      int32_t* st = stats + (size_t)e * 8;
-      for (int k = 0; k < 8; k++) st[k] = 0;
+      int32_t* st = stats + (size_t)e * 12;
+      for (int k = 0; k < 12; k++) st[k] = 0;
       for (int k = 0; k < m->task_frame_skip; k++) {
         step(m, &d);
         int nd = 0;
@@ -170,6 +171,7 @@ int or_step_stats(void* p, int n, const double* params, const double* action, do
         st[1] = d.nefc > st[1] ? d.nefc : st[1];
         st[2] = nd > st[2] ? nd : st[2];
         st[3] += d.solver_iter; st[4] += d.ls_iter; st[5] += d.noslip_iter; st[6] += 1;
+        st[8] += d.ncon; st[9] += d.nefc; st[10] += nd;
       }
       st[7] = (int32_t)d.status;
       store_state(m, &d, qpos + (size_t)e * m->nq, qvel + (size_t)e * m->nv, warm ? warm + (size_t)e * m->nv : nullptr);

@@ -114,13 +114,13 @@ class Oracle:
         return obs, rew, done.astype(bool), goal.astype(bool), status
 
     def step_stats(self, state: dict, action: np.ndarray, nthreads: int = 0):
-        """step() plus per-env work counts of the env-step: int32 [n, 8] = max ncon, max nefc, max
+        """step() plus per-env work counts of the env-step: int32 [n, 12] = max ncon, max nefc, max
         dense rows over the substeps, summed Newton iterations, line-search evaluations, noslip
-        sweeps, substeps, status flags"""
+        sweeps, substeps, status flags, summed ncon, nefc, dense rows, 0"""
         n = state["qpos"].shape[0]
         action = np.ascontiguousarray(action, np.float64).reshape(n, self.nu)
         obs = np.zeros((n, self.obs_dim)); rew = np.zeros(n)
-        done = np.zeros(n, np.uint8); goal = np.zeros(n, np.uint8); stats = np.zeros((n, 8), np.int32)
+        done = np.zeros(n, np.uint8); goal = np.zeros(n, np.uint8); stats = np.zeros((n, 12), np.int32)
         lib().or_step_stats(self.h, n, _p(state["params"]), _p(action), _p(state["qpos"]), _p(state["qvel"]),
                             _p(state["warm"]), _p(obs), _p(rew), _p(done, _u8p), _p(goal, _u8p),
                             stats.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), nthreads)

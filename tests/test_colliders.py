@@ -157,18 +157,27 @@ MPR_CASES = {
                                 CYL, np.zeros(3), rot_z(0.1), [0.02, 0.04, 0]),
     "sphere_on_cylinder_rim": (SPHERE, np.array([0.018, 0.0, 0.04 + 0.009]), I3, [0.01, 0, 0],
                                CYL, np.zeros(3), I3, [0.02, 0.04, 0]),
+    # line contacts: MPR's point is ill-conditioned along the line (any point of the overlap is a
+    # valid contact point; 1e-7 rad of rotation moves it to the other end)
+    "cylinder_lying_on_box": (CYL, np.array([0.05, 0.01, 0.05 + 0.02 - 0.002]), rot_y(np.pi / 2), [0.02, 0.04, 0],
+                              BOX, np.zeros(3), I3, BOXSZ),
+    "hammer_head_on_table": (CYL, np.array([-0.02, 0.03, 0.05 + 0.0245 - 0.0015]), rot_z(0.7) @ rot_y(np.pi / 2),
+                             [0.0245, 0.04, 0], BOX, np.zeros(3), I3, BOXSZ),
+    "capsule_across_cylinder_face": (CAP, np.array([0.0, 0.005, 0.04 + 0.01 - 0.001]), rot_y(np.pi / 2),
+                                     [0.01, 0.03, 0], CYL, np.zeros(3), I3, [0.02, 0.04, 0]),
 }
 
 
 @pytest.mark.gpu
 def test_gpu_mpr_pairs_match_oracle():
     """MPR (cylinder) pairs through the GPU narrowphase hook against the oracle's fp64 MPR, on
-    poses rounded to fp32 first (the kernel's inputs), contact by contact in emission order.
-    Point contacts only: MPR's contact point on a line / face contact is ill-conditioned (a capsule
-    lying across a cylinder's face: any point of the overlap line; GPU and oracle differ by 2e-3
-    along it while depth and normal agree).  Depth to 1e-5, normal to 1e-4, the point to 5e-4 --
-    MPR stops at mpr_tolerance, and the oracle's own point moves by up to 1e-4 under a 1e-7 rad
-    rotation of these inputs."""
+    identical inputs (poses and margin rounded to fp32 first: the kernel's inputs), contact by
+    contact in emission order, on the kernel's fp64 results before their fp32 rounding.  The
+    kernel's MPR follows libccd's operation order as the oracle states it (no contraction, 1 / sqrt
+    normalisation, aw_collide.h namespace mpr), so depth, normal AND point agree to 1e-12 -- also on
+    the line contacts (a cylinder lying on a box, the hammer head on the table, DAPG_hammer.xml:102;
+    a capsule across a cylinder's face), where the point is ill-conditioned along the line and any
+    difference in rounding moves it (round 4: 2e-3 apart with a different operation order)."""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -183,12 +192,15 @@ def test_gpu_mpr_pairs_match_oracle():
     pos = [[c[1], c[5]] for c in cases]
     mat = [[c[2].ravel(), c[6].ravel()] for c in cases]
     size = [[c[3], c[7]] for c in cases]
-    res = sim.collide_test(types, pos, mat, size, [5e-4] * len(names))
+    margin = float(np.float32(5e-4))
+    res = sim.collide_test(types, pos, mat, size, [margin] * len(names), fp64=True)
+    res32 = sim.collide_test(types, pos, mat, size, [margin] * len(names))
     _, o = make_oracle("hammer-v0")
-    for k, c, out in zip(names, cases, res):
-        ref = o.collide(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], 5e-4)
+    for k, c, out, out32 in zip(names, cases, res, res32):
+        ref = o.collide(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], margin)
         assert len(ref) >= 1, k                     # every case is a penetrating contact
         assert out.shape == ref.shape, (k, out, ref)
-        np.testing.assert_allclose(out[:, 0], ref[:, 0], atol=1e-5, err_msg=k)       # depth
-        np.testing.assert_allclose(out[:, 4:7], ref[:, 4:7], atol=1e-4, err_msg=k)   # normal
-        np.testing.assert_allclose(out[:, 1:4], ref[:, 1:4], atol=5e-4, err_msg=k)   # point
+        err = np.abs(out - ref).max()
+        print(f"{k}: {len(ref)} contact(s), max |GPU fp64 - oracle| = {err:.2e}")
+        np.testing.assert_allclose(out, ref, rtol=0, atol=1e-12, err_msg=k)   # depth, point, normal
+        np.testing.assert_allclose(out32, ref, rtol=0, atol=1e-7, err_msg=k)  # the fp32 contact the solver gets

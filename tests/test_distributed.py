@@ -113,6 +113,40 @@ def test_bench_launcher_dry_run_world2():
     assert x["summary"]["episodes"] == int((g % 3).sum())
 
 
+def test_bench_launcher_strong_scaling_shards():
+    """--gpus 2 --total-envs 262144 (SURVEY C4's strong-scaling total): 131 072 envs per rank at
+    global offsets 0 and 131 072, the exchange over both ranks' blocks."""
+    p = _bench("--gpus", "2", "--dry-run", "--total-envs", "262144")
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    d = json.loads(lines[0])
+    ranks = sorted(d["ranks"], key=lambda r: r["rank"])
+    assert [(r["env_offset"], r["envs"]) for r in ranks] == [(0, 131072), (131072, 131072)]
+    assert d["config"]["total_envs"] == 262144 and d["config"]["envs_per_gpu"] == 131072
+    x = d["exchange"]
+    assert x["episodes_ok"] and x["returns_ok"] and x["successes_ok"]
+    assert x["bytes_per_rank_per_call"] == 3 * 4 * 131072
+
+
+def test_count_gpus_without_hip(monkeypatch):
+    """The launcher parent counts GPUs through AMD SMI / the KFD topology, never a HIP call, and
+    applies the visibility variables; with neither source it raises instead of guessing."""
+    from mj_envs_amd import dist
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1")
+    assert dist._visible(8) == 2
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "3")
+    assert dist._visible(8) == 1
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES")
+    try:
+        n = dist.count_gpus()
+        assert n >= 0
+    except RuntimeError as e:
+        assert "neither" in str(e)
+    import torch
+    assert not torch.cuda.is_initialized()
+
+
 def test_bench_launcher_refuses_missing_gpus():
     """Never a silent fall-back to fewer ranks: with fewer visible GPUs than --gpus it exits non-zero."""
     import torch

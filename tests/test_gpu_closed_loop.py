@@ -57,7 +57,7 @@ def _sticky(sim, n):
 
 # --------------------------------------------------------------------------------------------
 # expected success (%) of the pretrained policies in this physics (oracle, 32 envs,
-# profiles/work_counts_*_dapg.json): the band the GPU rate must also fall in
+# profiles/dapg_oracle_*.json): the band the GPU rate must also fall in
 DAPG_MIN_SUCCESS = {"hammer-v0": 90.0, "pen-v0": 80.0, "relocate-v0": 90.0}
 
 

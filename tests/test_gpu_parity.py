@@ -111,26 +111,41 @@ def _no_overflow(sim, n):
     assert not (st & _native.ST_OVERFLOW).any(), f"{int(((st & _native.ST_OVERFLOW) != 0).sum())} envs overflowed"
 
 
-def _discrete_event(env_id, variation, o, params, qpos, qvel, warm, act, frame_skip, tol=1e-6):
+def _discrete_event(env_id, variation, o, params, qpos, qvel, warm, act, frame_skip, tol=1e-6, why=None):
     """Was this env-step decided by a discrete event?  Replays the oracle substep by substep and
     runs the GPU forward (aw_forward_dump) on each oracle substep state: True when at some
-    substep the two disagree on the contact set / constraint rows, or a contact lies within `tol`
-    of its activation margin (fp32 geometry decides such a contact on rounding)."""
+    substep the two disagree on the contact set / constraint rows, a contact lies within `tol`
+    of its activation margin (fp32 geometry decides such a contact on rounding), or the Newton
+    solves end with a row in a different activation state (a contact row quadratic on one side and
+    satisfied on the other, a frictionloss row sticking on one side and sliding on the other: the
+    stick-slip switch of mj_solNewton's piecewise-quadratic cost).  `why` (a list) receives the
+    reason."""
     from mj_envs_amd.tasks import attach_task, load_model
     from mj_envs_amd import _native
     m = attach_task(load_model(env_id), env_id, variation)
     one = _native.Sim(m.to_blob(), 1)
     ctrl = m.task_act_mid + np.clip(act, -1, 1) * m.task_act_rng
     q, v, w = qpos.copy(), qvel.copy(), warm.copy()
-    for _ in range(frame_skip):
+    note = why.append if why is not None else (lambda x: None)
+    for j in range(frame_skip):
         o.forward1(params, q, v, w, ctrl)
         sc = o.get("scalars")
         c = o.get("contact").reshape(-1, 23)
         one.set_state(_t(q[None]), _t(v[None]), _t(w[None]), _t(np.asarray(params)[None]))
         d = one.forward_dump(0, _t(ctrl))
         if d["ncon"] != int(sc[0]) or d["nefc"] != int(sc[1]):
+            note(f"substep {j}: contact / row set (ncon {d['ncon']} vs {int(sc[0])}, nefc {d['nefc']} vs {int(sc[1])})")
             return True
         if len(c) and np.min(np.abs(c[:, 0] - c[:, 17])) < tol:
+            note(f"substep {j}: contact at its margin")
+            return True
+        ost = o.get("efc_state").astype(int)
+        gst = d["efc_state"].astype(int)
+        if d["nefc"] and (gst != ost).any():
+            r = np.nonzero(gst != ost)[0]
+            ty = o.get("efc_type").astype(int)
+            note(f"substep {j}: Newton row states differ at rows {r.tolist()} (types {ty[r].tolist()}, "
+                 f"GPU {gst[r].tolist()} vs oracle {ost[r].tolist()})")
             return True
         o.mjstep1(params, q, v, w, ctrl, 1)
     return False
@@ -268,13 +283,19 @@ def _classify_misses(env_id, misses, frame_skip, variation=None):
         return []
     o = make_oracle(env_id, variation)[1]
     out = []
+    kinds = {}
     for ms in misses:
         (k, e, params, q, v, w, a), gpu = ms[:7], (ms[7:9] if len(ms) >= 9 else None)
-        if _discrete_event(env_id, variation, o, params, q, v, w, a, frame_skip):
+        why = []
+        if _discrete_event(env_id, variation, o, params, q, v, w, a, frame_skip, why=why):
+            key = why[0].split(": ", 1)[1].split(" (")[0].split(" at rows")[0] if why else "discrete"
+            kinds[key] = kinds.get(key, 0) + 1
             continue
         if _fp32_sensitive(o, params, q, v, w, a, env_id, variation, gpu=gpu):
+            kinds["fp32-sensitive reference"] = kinds.get("fp32-sensitive reference", 0) + 1
             continue
         out.append((k, e))
+    print(f"miss classes: {kinds}")
     return out
 
 

@@ -117,7 +117,7 @@ def test_oracle_dapg_policies_behave_as_published(env_id):
     pretrained DAPG policies (tests/golden/dapg_*.npz, mean actions as algos/baselines.py:82-86)
     solve hammer / pen / relocate in the oracle at MuJoCo's capacities (nconmax 100 / njmax 500);
     door-v0 runs at the reference's frame_skip 1 (door_v0.py:10), 5x finer than the policy was
-    trained at, and fails.  profiles/work_counts_*_dapg.json: 32 envs."""
+    trained at, and fails.  profiles/dapg_oracle_*.json: 32 envs."""
     import os
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))

@@ -35,7 +35,7 @@ def main(env_id="relocate-v0", n=4096, steps=200, threads=8, seed=0):
     for t in range(steps):
         act = rng.uniform(-1, 1, (n, o.nu))
         _, _, _, _, s = o.step_stats(st, act, nthreads=threads)
-        mx = np.maximum(mx, s[:, :3])
+        mx = np.maximum(mx, s[:, :3])   # per env: max ncon, nefc, dense rows of the env-step
     keys = ("ncon", "nefc", "ndense")
     out = dict(env_id=env_id, n_envs=n, steps=steps, seed=seed, wall_s=round(time.time() - t0, 1),
                caps_oracle=dict(ncon=o.max_con, nefc=o.max_efc), fast_caps=FAST_CAPS,

@@ -4,9 +4,9 @@ Drives the fp64 oracle with the reference's pretrained DAPG policies (tests/gold
 extracted by tests/golden/make_dapg.py) using the policy mean, exactly as the reference's
 evaluation does (``algos/baselines.py:82-86`` ``get_action(o)[1]['evaluation']``), and logs
   * the success rate (``evaluate_success``: > 25 goal steps, pen > 20; ``hammer_v0.py:167-175``),
-  * per-substep work counts with MuJoCo's capacities nconmax 100 / njmax 500
-    (``DAPG_assets.xml:4``): max / mean ncon, nefc, dense rows.
-Output: profiles/work_counts_<task>_dapg.json
+  * overflow at MuJoCo's capacities nconmax 100 / njmax 500 (``DAPG_assets.xml:4``).
+(The DAPG regime's per-substep work counts come from tools/work_counts.py ... dapg.)
+Output: profiles/dapg_oracle_<task>.json
     python tools/dapg_rollout.py [env_id|all] [n_envs] [seed]
 """
 import json
@@ -35,7 +35,7 @@ def policy_mean(p, obs):
     return x * p["out_scale"] + p["out_shift"]
 
 
-def rollout(env_id, n=32, seed=0, counts=True, max_con=100, max_efc=500):
+def rollout(env_id, n=32, seed=0, counts=False, max_con=100, max_efc=500):
     m = attach_task(load_model(env_id), env_id)
     o = Oracle(m.to_blob())
     o.set_option(max_con=max_con, max_efc=max_efc)
@@ -84,7 +84,7 @@ def main(which="all", n=32, seed=0):
         t0 = time.time()
         out = rollout(env_id, n, seed)
         out["wall_s"] = round(time.time() - t0, 1)
-        path = os.path.join(REPO, "profiles", f"work_counts_{env_id.split('-')[0]}_dapg.json")
+        path = os.path.join(REPO, "profiles", f"dapg_oracle_{env_id.split('-')[0]}.json")
         with open(path, "w") as f:
             json.dump(out, f, indent=1)
         print(json.dumps(out), flush=True)

@@ -121,6 +121,15 @@ def main(env_id="hammer-v0", pol_kind="dapg", steps=80, n=64, max_cases=12, dsbl
                         diff[ty] = dict(gpu=int((gt == ty).sum()), oracle=int((ot == ty).sum()),
                                         oracle_rows=[(int(i), float(pp)) for i, pp in zip(oi[ot == ty], op[ot == ty])])
                 sub["row_types_differ"] = diff
+            if d["nefc"] == int(sc[1]) and d["nefc"]:
+                ost, gst = o.get("efc_state").astype(int), d["efc_state"].astype(int)
+                if (ost != gst).any():
+                    ty, of = o.get("efc_type").astype(int), o.get("efc_force")
+                    ofl = o.get("efc_frictionloss")
+                    sub["row_states_differ"] = [dict(row=int(r), type=int(ty[r]), gpu=int(gst[r]), oracle=int(ost[r]),
+                                                     force_gpu=float(d["efc_force"][r]), force_oracle=float(of[r]),
+                                                     frictionloss=float(ofl[r]))
+                                                for r in np.nonzero(ost != gst)[0][:8]]
             if ocs != gcs and (len(ocs) != len(gcs) or any(abs(x[1] - y[1]) > 2e-5 for x, y in zip(ocs, gcs))
                                or any(x[0] != y[0] for x, y in zip(ocs, gcs))):
                 sub["contacts_gpu"] = gcs
@@ -152,7 +161,7 @@ def main(env_id="hammer-v0", pol_kind="dapg", steps=80, n=64, max_cases=12, dsbl
                 sub["qM"] = rel(d["qM"], o.get("qM").reshape(len(oq), len(oq)))
             rec["substeps"].append(sub)
             o.mjstep1(pre["params"], qp, qv, wm, ctrl, 1)
-            if rq > 2e-3 or "contacts_gpu" in sub:
+            if rq > 2e-3 or "contacts_gpu" in sub or "row_states_differ" in sub:
                 break
         report.append(rec)
         print(json.dumps(rec), flush=True)
