@@ -450,11 +450,12 @@ AW_DEV bool fast_overflow(const DModel& m, const Env& s) { return !WIDE && ((s.s
 // retry and the reset forward through it), which keeps the code object small enough for the
 // instruction cache.  Fast tier (defer != nullptr): a forward that overflows the fast capacities
 // abandons the env-step before anything is written and queues it for the wide tier (or, in the
-// reset forward, queues that forward alone).
+// reset forward, queues that forward alone).  kind DK_FORWARD (wide tier): only mj_forward + obs of
+// the stored state with ctrl 0 -- the reset forward's path through the same loop.
 template <int TASK>
 AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lane,
                      const float* __restrict__ actions, float* obs, float* reward, uint8_t* done, uint8_t* goal,
-                     float* terminal_obs, int autoreset, uint64_t seed, int* defer) {
+                     float* terminal_obs, int autoreset, uint64_t seed, int* defer, int kind = DK_STEP) {
   constexpr int NV = Tree<TASK>::NV;
   wsync();
   AW_PROF_START(s);
@@ -465,8 +466,9 @@ AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lan
     load_env<NV>(m, s, st, env, el);
     if (WIDE && el == 0) s.status = ST_WIDE;
     if (el < m.nu) {
-      float a = clampf(actions[(size_t)env * m.nu + el], -1.f, 1.f);
-      s.ctrl[el] = MD(act_mid, el) + a * MD(act_rng, el);
+      float c = 0.f;
+      if (kind == DK_STEP) c = MD(act_mid, el) + clampf(actions[(size_t)env * m.nu + el], -1.f, 1.f) * MD(act_rng, el);
+      s.ctrl[el] = c;
     }
     stage_model(m, s, st.params + (size_t)env * m.nparam, el);
   }
@@ -474,7 +476,7 @@ AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lan
   Dof d;
   float* ob = obs + (size_t)env * m.obs_dim;
   int sub = 0;
-  bool resetting = false, retry = false;
+  bool resetting = kind == DK_FORWARD, retry = false;
   AW_PROF(s, PR_PRE);
 #pragma nounroll
   while (true) {
@@ -552,8 +554,11 @@ AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lan
       if (rl == 0) st.status_acc[env] |= s.status & ~ST_OVF;
       defer_env(defer, env, DK_FORWARD, rl);
     } else {
-      write_obs(m, s, rl, ob);
-      if (rl == 0) st.status_acc[env] |= s.status;
+      if (obs) write_obs(m, s, rl, ob);
+      if (rl == 0) {
+        st.status_acc[env] |= s.status;
+        if (kind == DK_FORWARD) st.status[env] |= s.status;
+      }
     }
   }
 #ifdef AW_STAGE_PROF
@@ -562,22 +567,6 @@ AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lan
   if (lane == 0)
     for (int i = 0; i < AW_NPROF; i++) atomicAdd(&g_stage_prof[i], s.prof_acc[i]);
 #endif
-}
-
-// mj_forward + obs of a stored state (wide tier, DK_FORWARD): ctrl 0, as after a reset / set_state
-template <int TASK>
-AW_DEV void forward_stored(const DModel& m, Env& s, const DState& st, int env, int lane, float* obs) {
-  constexpr int NV = Tree<TASK>::NV;
-  wsync();
-  load_env<NV>(m, s, st, env, lane);
-  if (lane == 0) s.status = ST_WIDE;
-  if (lane < m.nu) s.ctrl[lane] = 0.f;
-  stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
-  float Mrow[NV];
-  Dof d;
-  forward<TASK>(m, s, lane, Mrow, d);
-  if (obs) write_obs(m, s, lane, obs + (size_t)env * m.obs_dim);
-  if (lane == 0) { st.status[env] |= s.status; st.status_acc[env] |= s.status; }
 }
 
 #ifndef AW_WIDE
@@ -718,14 +707,21 @@ __global__ void __launch_bounds__(64) k_step_wide(const DModel* __restrict__ mpt
     int k = 0;
     if (lane == 0) k = atomicAdd(q + 1, 1);
     k = __builtin_amdgcn_readfirstlane(k);
+#ifdef AW_TRACE
+    if (lane == 0) printf("wide wg %d: claimed %d, q0 %d\n", (int)blockIdx.x, k, q[0]);
+#endif
     if (k >= q[0]) break;
     const int ent = q[2 + k];
     const int env = ent & 0x3fffffff, kind = ent >> 30;
-    if (kind == DK_STEP)
-      env_step<TASK>(m, s, st, env, lane, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, nullptr);
-    else
-      forward_stored<TASK>(m, s, st, env, lane, obs);
+#ifdef AW_TRACE
+    if (lane == 0) printf("wide wg %d claim %d of %d: env %d kind %d\n", (int)blockIdx.x, k, q[0], env, kind);
+#endif
+    env_step<TASK>(m, s, st, env, lane, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, nullptr,
+                   kind);
   }
+#ifdef AW_TRACE
+  if (lane == 0) printf("wide wg %d: exit\n", (int)blockIdx.x);
+#endif
 }
 #endif  // AW_WIDE
 

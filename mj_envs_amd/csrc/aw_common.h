@@ -117,6 +117,11 @@ static_assert(PR_CS_J < AW_NPROF, "stage profiler ids");
   } while (0)
 #define AW_PROF_COUNT(S, ID) do { if (threadIdx.x == 0) (S).prof_acc[ID] += 1; } while (0)
 #define AW_PROF_ADD(S, ID, V) do { if (threadIdx.x == 0) (S).prof_acc[ID] += (unsigned long long)(V); } while (0)
+#elif defined(AW_TRACE)   // debugging builds: every stage boundary printed by lane 0 (device printf)
+#define AW_PROF_START(S) ((void)0)
+#define AW_PROF(S, ID) do { if (threadIdx.x == 0) printf("wg %d stage %d\n", (int)blockIdx.x, (int)(ID)); } while (0)
+#define AW_PROF_COUNT(S, ID) ((void)0)
+#define AW_PROF_ADD(S, ID, V) ((void)0)
 #else
 #define AW_PROF_START(S) ((void)0)
 #define AW_PROF(S, ID) ((void)0)

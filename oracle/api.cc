@@ -136,7 +136,7 @@ int or_step(void* p, int n, const double* params, const double* action, double* 
 /* or_step + per-env work counts of the env-step (test / profiling hook, tools/work_counts.py):
  * stats[e][12] = max ncon, max nefc, max dense (contact) rows over the frame_skip substeps, summed
  * Newton iterations, line-search derivative evaluations and noslip sweeps, substeps, status, summed
- * ncon, nefc and dense rows, 0 */
+ * ncon, nefc and dense rows, substeps with a box-box contact */
 int or_step_stats(void* p, int n, const double* params, const double* action, double* qpos, double* qvel,
                   double* warm, double* obs, double* reward, uint8_t* done, uint8_t* goal, int32_t* stats,
                   int nthreads) {
@@ -172,6 +172,10 @@ int or_step_stats(void* p, int n, const double* params, const double* action, do
         st[2] = nd > st[2] ? nd : st[2];
         st[3] += d.solver_iter; st[4] += d.ls_iter; st[5] += d.noslip_iter; st[6] += 1;
         st[8] += d.ncon; st[9] += d.nefc; st[10] += nd;
+        int bb = 0;
+        for (int c = 0; c < d.ncon; c++)
+          bb |= m->geom_type[d.contact[c].geom1] == GEOM_BOX && m->geom_type[d.contact[c].geom2] == GEOM_BOX;
+        st[11] += bb;
       }
       st[7] = (int32_t)d.status;
       store_state(m, &d, qpos + (size_t)e * m->nq, qvel + (size_t)e * m->nv, warm ? warm + (size_t)e * m->nv : nullptr);

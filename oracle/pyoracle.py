@@ -116,7 +116,7 @@ class Oracle:
     def step_stats(self, state: dict, action: np.ndarray, nthreads: int = 0):
         """step() plus per-env work counts of the env-step: int32 [n, 12] = max ncon, max nefc, max
         dense rows over the substeps, summed Newton iterations, line-search evaluations, noslip
-        sweeps, substeps, status flags, summed ncon, nefc, dense rows, 0"""
+        sweeps, substeps, status flags, summed ncon, nefc, dense rows, substeps with a box-box contact"""
         n = state["qpos"].shape[0]
         action = np.ascontiguousarray(action, np.float64).reshape(n, self.nu)
         obs = np.zeros((n, self.obs_dim)); rew = np.zeros(n)

@@ -204,3 +204,73 @@ def test_gpu_mpr_pairs_match_oracle():
         print(f"{k}: {len(ref)} contact(s), max |GPU fp64 - oracle| = {err:.2e}")
         np.testing.assert_allclose(out, ref, rtol=0, atol=1e-12, err_msg=k)   # depth, point, normal
         np.testing.assert_allclose(out32, ref, rtol=0, atol=1e-7, err_msg=k)  # the fp32 contact the solver gets
+
+
+def _rot_x(a):
+    c, s = np.cos(a), np.sin(a)
+    return np.array([[1, 0, 0], [0, c, -s], [0, s, c]])
+
+
+# box-box through the GPU (fp32 SAT + face clipping, aw_collide.h c_box_box) vs the oracle's fp64
+# statement of the same construction: face on face (overlap corners), the Adroit palm box
+# (C_palm0, DAPG_Adroit.xml:11, half-sizes 0.032 0.0111 0.049) resting tilted on the table
+# (DAPG_relocate.xml:32), an edge across an edge, a corner into a face.
+BOXBOX_CASES = {
+    "face_on_face_overhang": (np.zeros(3), I3, BOXSZ, np.array([0.2, 0.0, 0.05 + 0.05 - 0.001]), I3,
+                              np.array([0.05, 0.05, 0.05])),
+    "palm_tilted_on_table": (np.zeros(3), I3, np.array([0.6, 0.6, 0.025]), None,
+                             rot_z(0.3) @ _rot_x(np.pi / 2 + 0.05), np.array([0.032, 0.0111, 0.049])),
+    "edge_across_edge": (np.zeros(3), I3, BOXSZ, None, rot_z(np.pi / 4) @ _rot_x(np.pi / 4),
+                         np.array([0.03, 0.03, 0.03])),
+    "corner_into_face": (np.zeros(3), I3, BOXSZ, None, rot_z(0.4) @ _rot_x(0.6) @ rot_y(0.5),
+                         np.array([0.02, 0.03, 0.025])),
+}
+
+
+def _boxbox_case(name):
+    p1, m1, s1, p2, m2, s2 = BOXBOX_CASES[name]
+    if p2 is None:                       # place the second box's lowest feature 0.001 below the top face
+        corners = np.array([[a, b, c] for a in (-1, 1) for b in (-1, 1) for c in (-1, 1)]) * s2
+        low = (corners @ m2.T)[:, 2].min()
+        x = 0.205 if name == "edge_across_edge" else 0.05
+        p2 = np.array([x, 0.01, s1[2] - low - 0.001])
+    return p1, m1, s1, p2, m2, s2
+
+
+@pytest.mark.gpu
+def test_gpu_boxbox_match_oracle():
+    """Box-box contacts of the GPU collider against the oracle, contact by contact in emission
+    order, on identical fp32-rounded inputs: depth, point and normal to 2e-6 (fp32 geometry)."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mj_envs_amd import _native
+    from mj_envs_amd.tasks import attach_task, load_model
+    m = attach_task(load_model("relocate-v0"), "relocate-v0")
+    sim = _native.Sim(m.to_blob(), 1)
+    names = sorted(BOXBOX_CASES)
+    f32 = lambda x: np.asarray(x, np.float32).astype(np.float64)
+    cases = [[f32(v) for v in _boxbox_case(k)] for k in names]
+    margin = float(np.float32(5e-4))
+    res = sim.collide_test([[BOX, BOX]] * len(names), [[c[0], c[3]] for c in cases],
+                           [[c[1].ravel(), c[4].ravel()] for c in cases], [[c[2], c[5]] for c in cases],
+                           [margin] * len(names))
+    _, o = make_oracle("relocate-v0")
+    for k, c, out in zip(names, cases, res):
+        ref = o.collide(BOX, c[0], c[1], c[2], BOX, c[3], c[4], c[5], margin)
+        print(f"{k}: {len(ref)} contact(s) oracle, {len(out)} GPU")
+        assert len(ref) >= 1, k
+        assert out.shape == ref.shape, (k, out, ref)
+        np.testing.assert_allclose(out, ref, rtol=0, atol=2e-6, err_msg=k)
+
+
+def test_boxbox_cases_have_contacts(orc):
+    """the box-box GPU cases are penetrating contacts of the intended kind (oracle)"""
+    _, o = orc
+    f32 = lambda x: np.asarray(x, np.float32).astype(np.float64)
+    for k in BOXBOX_CASES:
+        c = [f32(v) for v in _boxbox_case(k)]
+        out = o.collide(BOX, c[0], c[1], c[2], BOX, c[3], c[4], c[5], float(np.float32(5e-4)))
+        assert len(out) >= 1 and (out[:, 0] < 0).all(), (k, out)
+        if k == "face_on_face_overhang":
+            assert len(out) == 4

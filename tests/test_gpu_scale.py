@@ -173,6 +173,8 @@ def test_config3_full_size_16384_envs(env_id):
         misses += [(k, int(sel[j]), pre["params"][sel[j]], pre["qpos"][sel[j]], pre["qvel"][sel[j]], pre["warm"][sel[j]],
                     a[sel[j]], qg[j].astype(np.float64), vg[j].astype(np.float64)) for j in np.where(~okk)[0]]
         roks.append(_rewards_close(rew.cpu().numpy()[sel], r_ref, check=False))
+        if k % 25 == 0:
+            print(f"  {env_id} step {k}: {int(lw.sum())} wide-tier env-steps, {len(misses)} misses so far", flush=True)
     _, sticky = _status(sim, n)
     n_over = int(((sticky & _native.ST_OVERFLOW) != 0).sum())
     n_wide = int(((sticky & _native.ST_WIDE) != 0).sum())
@@ -238,6 +240,8 @@ def test_dapg_teacher_forced_headline_size():
         misses += [(warm_steps + k, int(idx[j]), pre["params"][j], pre["qpos"][j], pre["qvel"][j], pre["warm"][j],
                     a[j], qg[j].astype(np.float64), vg[j].astype(np.float64)) for j in np.where(~okk)[0]]
         roks.append(_rewards_close(rew.cpu().numpy()[idx], r_ref, check=False))
+        if k % 20 == 0:
+            print(f"  DAPG step {warm_steps + k}: {len(misses)} misses so far", flush=True)
     ok = np.concatenate(oks)
     frac, rfrac = ok.mean(), np.concatenate(roks).mean()
     label = f"DAPG headline size (hammer-v0, {n} envs, grid {sim.grid})"

@@ -51,7 +51,7 @@ def counts(env_id="hammer-v0", n=32, steps=200, policy="random", seed=0, threads
         over += int(((s[:, 7] & 24) != 0).sum())
     sub = float(tot[6])
     avg = dict(ncon=tot[8] / sub, nefc=tot[9] / sub, ndense=tot[10] / sub, newton_iter=tot[3] / sub,
-               noslip_iter=tot[5] / sub, ls_iter=tot[4] / max(tot[3], 1))
+               noslip_iter=tot[5] / sub, ls_iter=tot[4] / max(tot[3], 1), boxbox_substep_frac=tot[11] / sub)
     return dict(env_id=env_id, n_envs=n, steps=steps, seed=seed, substeps=int(sub),
                 policy="iid U(-1,1) actions" if pol is None else "DAPG pretrained (mean action)",
                 caps=dict(max_con=o.max_con, max_efc=o.max_efc), overflow_env_steps=over,
