@@ -148,7 +148,7 @@ def _miss_is_fp32_sensitive(o, o32, st, act, gpu=None, trials=8, ulps=16, seed=0
     return bool(okq and okv)
 
 
-def same_run_parity(blob, sim, n=256, model=None):
+def same_run_parity(blob, sim, n=256, model=None, pol=None, obs_now=None):
     """One env-step of the benchmark's OWN handle (all its envs, the timed run's launch
     configuration: persistent workgroups claiming envs past the resident slots) from its mid-run
     states, checked on n envs sampled evenly across the whole batch against the fp64 oracle from
@@ -162,7 +162,10 @@ def same_run_parity(blob, sim, n=256, model=None):
     q, v, w, p = sim.empty(N, sim.nq), sim.empty(N, sim.nv), sim.empty(N, sim.nv), sim.empty(N, sim.nparam)
     sim.get_state(q, v, w, p)
     act = sim.empty(N, sim.nu)
-    sim.random_actions(act, 12345, 0)
+    if pol is not None and obs_now is not None:
+        pol.act(obs_now, out=act)        # the closed loop's own (mean) action: the regime the bench timed
+    else:
+        sim.random_actions(act, 12345, 0)
     obs, rew = sim.empty(N, sim.obs_dim), sim.empty(N)
     done, goal = sim.empty(N, dtype=torch.uint8), sim.empty(N, dtype=torch.uint8)
     sim.step(act, obs, rew, done, goal)
@@ -535,7 +538,9 @@ def main():
                     episodes=episodes, exchange=exchange)
         if world == 1 and not args.no_parity:
             try:
-                line["parity_one_step"] = same_run_parity(blob, sim, model=m)
+                line["parity_one_step"] = same_run_parity(blob, sim, model=m, pol=pol, obs_now=obs)
+                line["parity_one_step"]["actions"] = ("the policy's mean action on the current obs" if pol is not None
+                                                      else "Philox U(-1, 1)")
             except Exception as e:
                 line["parity_one_step"] = dict(error=str(e))
         if world == 1 and env_id == ENV_ID and depth is None and pol is None and n == 65536 \

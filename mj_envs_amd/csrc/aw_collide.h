@@ -568,8 +568,11 @@ namespace mpr {
 // kernel's portal, depth, normal and point are then bitwise the oracle's -- including the line /
 // face contacts (a cylinder lying on a box), whose point is ill-conditioned along the line
 // (tests/test_colliders.py test_gpu_mpr_pairs_match_oracle).
-#ifndef AW_MPR_FAST
-#pragma clang fp contract(off)
+// every function body of this namespace starts with MPR_EXACT: no contraction in that scope
+#ifdef AW_MPR_FAST
+#define MPR_EXACT
+#else
+#define MPR_EXACT _Pragma("clang fp contract(off)")
 #endif
 // libccd's CCD_EPS of the matching build: DBL_EPSILON (MuJoCo's double build) / FLT_EPSILON
 template <class T> constexpr T EPS_T = sizeof(T) == 8 ? T(2.220446049250313e-16) : T(1.1920928955078125e-07);
@@ -578,36 +581,36 @@ template <class T> struct GVdT {
   int type;
 };
 // local vector helpers (compiled under the pragma above: no contraction)
-template <class T> AW_DEV T dot3(const T* a, const T* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-template <class T> AW_DEV void cross3(T* r, const T* a, const T* b) {
+template <class T> AW_DEV T dot3(const T* a, const T* b) { MPR_EXACT return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+template <class T> AW_DEV void cross3(T* r, const T* a, const T* b) { MPR_EXACT
   T t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
   r[0] = t0; r[1] = t1; r[2] = t2;
 }
-template <class T> AW_DEV void sub3(T* r, const T* a, const T* b) { r[0] = a[0] - b[0]; r[1] = a[1] - b[1]; r[2] = a[2] - b[2]; }
-template <class T> AW_DEV void add3(T* r, const T* a, const T* b) { r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2]; }
-template <class T> AW_DEV void scl3(T* r, const T* a, T s) { r[0] = a[0] * s; r[1] = a[1] * s; r[2] = a[2] * s; }
-template <class T> AW_DEV void copy3(T* r, const T* a) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; }
-template <class T> AW_DEV void mulmv3(T* r, const T* m, const T* v) {
+template <class T> AW_DEV void sub3(T* r, const T* a, const T* b) { MPR_EXACT r[0] = a[0] - b[0]; r[1] = a[1] - b[1]; r[2] = a[2] - b[2]; }
+template <class T> AW_DEV void add3(T* r, const T* a, const T* b) { MPR_EXACT r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2]; }
+template <class T> AW_DEV void scl3(T* r, const T* a, T s) { MPR_EXACT r[0] = a[0] * s; r[1] = a[1] * s; r[2] = a[2] * s; }
+template <class T> AW_DEV void copy3(T* r, const T* a) { MPR_EXACT r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; }
+template <class T> AW_DEV void mulmv3(T* r, const T* m, const T* v) { MPR_EXACT
   T t0 = m[0] * v[0] + m[1] * v[1] + m[2] * v[2];
   T t1 = m[3] * v[0] + m[4] * v[1] + m[5] * v[2];
   T t2 = m[6] * v[0] + m[7] * v[1] + m[8] * v[2];
   r[0] = t0; r[1] = t1; r[2] = t2;
 }
-template <class T> AW_DEV void mulmtv3(T* r, const T* m, const T* v) {
+template <class T> AW_DEV void mulmtv3(T* r, const T* m, const T* v) { MPR_EXACT
   T t0 = m[0] * v[0] + m[3] * v[1] + m[6] * v[2];
   T t1 = m[1] * v[0] + m[4] * v[1] + m[7] * v[2];
   T t2 = m[2] * v[0] + m[5] * v[1] + m[8] * v[2];
   r[0] = t0; r[1] = t1; r[2] = t2;
 }
-template <class T> AW_DEV bool is_zero(T x) { return fabs(x) < EPS_T<T>; }
-template <class T> AW_DEV bool eq(T a, T b) {
+template <class T> AW_DEV bool is_zero(T x) { MPR_EXACT return fabs(x) < EPS_T<T>; }
+template <class T> AW_DEV bool eq(T a, T b) { MPR_EXACT
   T ab = fabs(a - b);
   if (ab < EPS_T<T>) return true;
   T fa = fabs(a), fb = fabs(b);
   return fb > fa ? ab < EPS_T<T> * fb : ab < EPS_T<T> * fa;
 }
-template <class T> AW_DEV bool veq(const T* a, const T* b) { return eq(a[0], b[0]) && eq(a[1], b[1]) && eq(a[2], b[2]); }
-template <class T> AW_DEV void vnorm(T* v) {
+template <class T> AW_DEV bool veq(const T* a, const T* b) { MPR_EXACT return eq(a[0], b[0]) && eq(a[1], b[1]) && eq(a[2], b[2]); }
+template <class T> AW_DEV void vnorm(T* v) { MPR_EXACT
 #ifdef AW_MPR_FAST
   T k = rsqrt_fast(dot3(v, v));
 #else
@@ -615,14 +618,14 @@ template <class T> AW_DEV void vnorm(T* v) {
 #endif
   scl3(v, v, k);
 }
-template <class T> AW_DEV T sgn(T x) { return x < 0 ? -T(1.0) : (x > 0 ? T(1.0) : T(0.0)); }
+template <class T> AW_DEV T sgn(T x) { MPR_EXACT return x < 0 ? -T(1.0) : (x > 0 ? T(1.0) : T(0.0)); }
 
 template <class T> struct SupT { T v[3], v1[3], v2[3]; };
 
 // support point of a primitive in direction dir (world), inflated by margin / 2.  Branch-free:
 // the lanes of one MPR round hold pairs of different geom types, and a type switch would run
 // every shape's branch in turn.
-template <class T> AW_DEV void gsupport(T* res, const GVdT<T>& g, const T* dir, T margin) {
+template <class T> AW_DEV void gsupport(T* res, const GVdT<T>& g, const T* dir, T margin) { MPR_EXACT
   T ld[3], r[3];
   mulmtv3(ld, g.mat, dir);
   const T* s = g.size;
@@ -654,7 +657,7 @@ template <class T> AW_DEV void gsupport(T* res, const GVdT<T>& g, const T* dir, 
 // within the lane pair, and both lanes run the rest of MPR identically -- the same arithmetic as one
 // lane evaluating both supports, half the support work on the chain and half the geometry
 // registers (r04s A/B: -1.9 % random, -0.4 % DAPG)
-AW_DEV double swap_pair(double x) {
+AW_DEV double swap_pair(double x) { MPR_EXACT
   const long long b = __builtin_bit_cast(long long, x);
   const int lo = __builtin_amdgcn_update_dpp((int)b, (int)b, 0xB1, 0xF, 0xF, false);
   const int hi = __builtin_amdgcn_update_dpp((int)(b >> 32), (int)(b >> 32), 0xB1, 0xF, 0xF, false);
@@ -662,7 +665,7 @@ AW_DEV double swap_pair(double x) {
 }
 template <class T> struct Ctx { const GVdT<T>* own; int half; T opos[3]; T margin, tol; int maxit; };
 
-template <class T> AW_DEV void support(const Ctx<T>& c, const T* dir, SupT<T>& s) {
+template <class T> AW_DEV void support(const Ctx<T>& c, const T* dir, SupT<T>& s) { MPR_EXACT
   T d[3], r[3], o[3];
   scl3(d, dir, c.half ? T(-1) : T(1));
   gsupport(r, *c.own, d, c.margin);
@@ -677,24 +680,24 @@ template <class T> AW_DEV void support(const Ctx<T>& c, const T* dir, SupT<T>& s
 // the portal is kept as four named vertices (no array) so every vertex stays in VGPRs
 template <class T> struct PortalT { SupT<T> p0, p1, p2, p3; };
 // element-wise copy (a whole-struct copy becomes a memcpy that keeps the portal in scratch)
-template <class T> AW_DEV void setsup(SupT<T>& d, const SupT<T>& s) {
+template <class T> AW_DEV void setsup(SupT<T>& d, const SupT<T>& s) { MPR_EXACT
 #pragma unroll
   for (int k = 0; k < 3; k++) { d.v[k] = s.v[k]; d.v1[k] = s.v1[k]; d.v2[k] = s.v2[k]; }
 }
 
-template <class T> AW_DEV void portal_dir(const PortalT<T>& P, T* dir) {
+template <class T> AW_DEV void portal_dir(const PortalT<T>& P, T* dir) { MPR_EXACT
   T a[3], b[3];
   sub3(a, P.p2.v, P.p1.v);
   sub3(b, P.p3.v, P.p1.v);
   cross3(dir, a, b);
   vnorm(dir);
 }
-template <class T> AW_DEV bool reach_tol(const PortalT<T>& P, const SupT<T>& v4, const T* dir, T tol) {
+template <class T> AW_DEV bool reach_tol(const PortalT<T>& P, const SupT<T>& v4, const T* dir, T tol) { MPR_EXACT
   T dv1 = dot3(P.p1.v, dir), dv2 = dot3(P.p2.v, dir), dv3 = dot3(P.p3.v, dir), dv4 = dot3(v4.v, dir);
   T d1 = fmin(fmin(dv4 - dv1, dv4 - dv2), dv4 - dv3);
   return eq(d1, tol) || d1 < tol;
 }
-template <class T> AW_DEV void selsup(SupT<T>& d, bool c, const SupT<T>& s) {
+template <class T> AW_DEV void selsup(SupT<T>& d, bool c, const SupT<T>& s) { MPR_EXACT
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     d.v[k] = c ? s.v[k] : d.v[k]; d.v1[k] = c ? s.v1[k] : d.v1[k]; d.v2[k] = c ? s.v2[k] : d.v2[k];
@@ -702,7 +705,7 @@ template <class T> AW_DEV void selsup(SupT<T>& d, bool c, const SupT<T>& s) {
 }
 // branch-free vertex replacement: conditional struct stores through a selected pointer would
 // pin the portal in scratch
-template <class T> AW_DEV void expand(PortalT<T>& P, const SupT<T>& v4) {
+template <class T> AW_DEV void expand(PortalT<T>& P, const SupT<T>& v4) { MPR_EXACT
   T v4v0[3];
   cross3(v4v0, v4.v, P.p0.v);
   const bool a1 = dot3(P.p1.v, v4v0) > 0;
@@ -712,7 +715,7 @@ template <class T> AW_DEV void expand(PortalT<T>& P, const SupT<T>& v4) {
   selsup(P.p3, a1 && !a2, v4);
   selsup(P.p2, !a1 && a3, v4);
 }
-template <class T> AW_DEV int discover(const Ctx<T>& c, PortalT<T>& P) {
+template <class T> AW_DEV int discover(const Ctx<T>& c, PortalT<T>& P) { MPR_EXACT
   T dir[3], va[3], vb[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) {
@@ -765,7 +768,7 @@ template <class T> AW_DEV int discover(const Ctx<T>& c, PortalT<T>& P) {
   }
   return -1;
 }
-template <class T> AW_DEV int refine(const Ctx<T>& c, PortalT<T>& P) {
+template <class T> AW_DEV int refine(const Ctx<T>& c, PortalT<T>& P) { MPR_EXACT
   T dir[3];
   SupT<T> v4;
   for (int it = 0; it <= c.maxit; it++) {
@@ -779,7 +782,7 @@ template <class T> AW_DEV int refine(const Ctx<T>& c, PortalT<T>& P) {
   }
   return -1;
 }
-template <class T> AW_DEV T pseg2(const T* P, const T* x0, const T* b, T* w) {
+template <class T> AW_DEV T pseg2(const T* P, const T* x0, const T* b, T* w) { MPR_EXACT
   T dd[3], a[3];
   sub3(dd, b, x0);
   sub3(a, x0, P);
@@ -793,7 +796,7 @@ template <class T> AW_DEV T pseg2(const T* P, const T* x0, const T* b, T* w) {
   }
   return dot3(df, df);
 }
-template <class T> AW_DEV T ptri2(const T* P, const T* x0, const T* B, const T* C, T* w) {
+template <class T> AW_DEV T ptri2(const T* P, const T* x0, const T* B, const T* C, T* w) { MPR_EXACT
   T d1[3], d2[3], a[3];
   sub3(d1, B, x0);
   sub3(d2, C, x0);
@@ -823,7 +826,7 @@ template <class T> AW_DEV T ptri2(const T* P, const T* x0, const T* B, const T* 
   for (int k = 0; k < 3; k++) w[k] = take ? w2[k] : w[k];
   return dist;
 }
-template <class T> AW_DEV void find_pos(const PortalT<T>& P, T* pos) {
+template <class T> AW_DEV void find_pos(const PortalT<T>& P, T* pos) { MPR_EXACT
   T dir[3], vec[3], b0, b1, b2, b3;
   portal_dir(P, dir);
   cross3(vec, P.p1.v, P.p2.v); b0 = dot3(vec, P.p3.v);
@@ -846,7 +849,7 @@ template <class T> AW_DEV void find_pos(const PortalT<T>& P, T* pos) {
     pos[k] = T(0.5) * (p1 + p2) * inv;
   }
 }
-template <class T> AW_DEV int penetration(const Ctx<T>& c, T* depth, T* dir, T* pos) {
+template <class T> AW_DEV int penetration(const Ctx<T>& c, T* depth, T* dir, T* pos) { MPR_EXACT
   PortalT<T> P;
   int res = discover(c, P);
   if (res < 0) return -1;
@@ -880,9 +883,7 @@ template <class T> AW_DEV int penetration(const Ctx<T>& c, T* depth, T* dir, T* 
     expand(P, v4);
   }
 }
-#ifndef AW_MPR_FAST
-#pragma clang fp contract(fast)
-#endif
+#undef MPR_EXACT
 }  // namespace mpr
 
 // fp64 pose of collidable geom g from the fp64 body frames (stage_kin64), as the oracle's

@@ -107,13 +107,18 @@ class AdroitVecEnv:
         return out
 
     def mj_viewer_headless_setup(self, width: Optional[int] = None, height: Optional[int] = None,
-                                 aerial: bool = False):
+                                 aerial: Optional[bool] = None):
         """``headless_observer.py:20-31`` (+ ``set_view``, ``:59-66``): the offscreen free camera
         (azimuth 90, distance 4.5, elevation from the observed body; ``aerial`` flips the
         elevation's sign as ``set_view('aerial')`` / pen's ``use_aerial_view`` do).  Here it builds
         the camera record every env of the batch is rendered from (``render.free_camera``) and
-        returns it; ``render_depth`` uses it from then on."""
+        returns it; ``render_depth`` uses it from then on.  ``aerial`` None: the single-env facade
+        this batch belongs to decides (pen_v0.py:174-177 reads its ``use_aerial_view``), so the
+        reference's ``gym_env.env.mj_viewer_headless_setup()`` through a wrapper keeps the flag."""
         from .render import free_camera
+        if aerial is None:
+            fac = getattr(self, "_facade", None)
+            aerial = bool(fac is not None and self.env_id == "pen-v0" and getattr(fac, "use_aerial_view", False))
         w, h = (width or self._cam_key[0], height or self._cam_key[1]) if getattr(self, "_cam_key", None) \
             else (width or 64, height or 64)
         self._aerial = bool(aerial)
@@ -201,6 +206,7 @@ class _AdroitEnv(_reference_base()):
         self.observer = None            # the camera record once mj_viewer_headless_setup() ran
         self.vec = AdroitVecEnv(self.env_id, 1, device=device, variation_type=variation_type,
                                 seed=1, autoreset=False)
+        self.vec._facade = self         # camera flags (pen's use_aerial_view) of this facade
         self.model = self.vec.model
         self.frame_skip = self.vec.frame_skip
         self.act_mid = self.vec.act_mid.astype(np.float64)

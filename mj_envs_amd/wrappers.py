@@ -49,7 +49,9 @@ class PixelObservationVecEnv:
                  action_repeat: int = 1, host_tensors: bool = False):
         if obs_key not in (PIXELS_KEY, STATE_KEY):
             raise KeyError(obs_key)
+        self._facade = None
         if not isinstance(env, AdroitVecEnv) and isinstance(getattr(env, "vec", None), AdroitVecEnv):
+            self._facade = env                # its flags (pen's use_aerial_view) stay reachable
             env = env.vec                     # a single-env facade: wrap its batch of one
         self.host_tensors = bool(host_tensors)
         rk = render_kwargs or {}
@@ -88,7 +90,8 @@ class PixelObservationVecEnv:
         return self.get_pixels() if self.obs_key == PIXELS_KEY else self.get_state()
 
     def mj_viewer_headless_setup(self):
-        """forwarded to the env, as gym's wrapper attribute lookup does for the reference"""
+        """forwarded to the env, as gym's wrapper attribute lookup does for the reference; a wrapped
+        single-env facade keeps its own flags (pen_v0.py:174-177 reads use_aerial_view)"""
         return self.env.mj_viewer_headless_setup(self.width, self.height)
 
     def _actions(self, actions):

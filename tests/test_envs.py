@@ -259,7 +259,11 @@ def test_record_policy_drives_facade(env_id):
     assert e.render().shape == (64, 64)
     if env_id == "pen-v0":
         e.use_aerial_view = True
-        assert not np.array_equal(e.mj_viewer_headless_setup(), cam)
+        aerial = e.mj_viewer_headless_setup()
+        assert not np.array_equal(aerial, cam)
+        # record_policy's call through the wrapper keeps the facade's flag
+        np.testing.assert_array_equal(gym_env.env.mj_viewer_headless_setup(), aerial)
+        np.testing.assert_array_equal(gym_env.mj_viewer_headless_setup(), aerial)
     gym_env.close()
 
 
