@@ -114,7 +114,7 @@ AW_DEV void sort_contacts(Env& s, int lane) {
       copy3(s.con_nrm[r], nrm[h]);
     }
   }
-  if (lane == 0) s.ncon = n;
+  if (lane == 0) s.ncon = n - (int)s.kin64_mask;   // fp64-dropped candidates sorted last (stage_collision)
   wsync();
 }
 
@@ -226,22 +226,58 @@ AW_DEV void stage_collision(const DModel& m, Env& s, int lane) {
     AW_PROF(s, PR_CO_C2);
     narrow_class<3>(m, s, plist, cnt[3], lane);
     AW_PROF(s, PR_CO_C3);
+    // contacts of the sphere / capsule classes within DEC_EPS of their margin (aw_collide.h): their
+    // activation is decided in fp64 below, so their bodies' fp64 frames are staged with the MPR ones
+    wsync();
+    const int nc0 = s.ncon < MAXCON ? s.ncon : MAXCON;
+    unsigned long long km = 0ull;
+    bool und[NCH];
+#pragma unroll
+    for (int h = 0; h < NCH; h++) {
+      const int c = lane + 64 * h;
+      und[h] = false;
+      if (c < nc0) {
+        const int pr = s.con_pair[c];
+        const int cls = MD(cp_pack, pr) & 0xff;
+        und[h] = (cls == 1 || cls == 2) && fabsf(s.con_dist[c] - MD(cp_margin, pr)) <= DEC_EPS;
+        if (und[h]) km |= MD(cp_kin64, pr);
+      }
+    }
     // MPR (cylinder) pairs: the midphase first (fp32 frames, exact distance lower bounds), so
     // that only pairs that can touch request fp64 frames and run fp64 MPR (hammer: the upright
     // wall's bounding sphere covers the scene, 5 of its 6 broadphase survivors never touch)
     if (cnt[4] > 0) cnt[4] = midphase<4>(m, s, plist + m.cls_start[4], cnt[4], lane);
-    if (cnt[4] > 0) {
-      // the surviving MPR pairs' body closures: only those frames are computed in fp64
+    // the surviving MPR pairs' body closures: only those frames are computed in fp64
+    for (int i = lane; i < cnt[4]; i += 64) km |= MD(cp_kin64, plist[m.cls_start[4] + i]);
+    if (__ballot(km != 0ull)) {
       if (lane == 0) s.kin64_mask = 0ull;
       wsync();
-      unsigned long long km = 0ull;
-      for (int i = lane; i < cnt[4]; i += 64) km |= MD(cp_kin64, plist[m.cls_start[4] + i]);
       if (km) atomicOr(&s.kin64_mask, km);
       wsync();
       stage_kin64(m, s, lane);
       AW_PROF(s, PR_CO_KIN64);
-      narrow_class<4>(m, s, plist, cnt[4], lane);
+      if (cnt[4] > 0) narrow_class<4>(m, s, plist, cnt[4], lane);
+      // fp64 activation: drop a candidate beyond its margin (its key moves past every valid key, so
+      // the sort puts it last and cuts it), keep the others with their fp64 distance
+      int ndrop = 0;
+#pragma unroll
+      for (int h = 0; h < NCH; h++) {
+        const int c = lane + 64 * h;
+        bool drop = false;
+        if (und[h]) {
+          const double d64 = contact_dist64(m, s, c);
+          drop = d64 > MD(cp_margin64, s.con_pair[c]);
+          if (drop) s.con_key[c] = 0x7fff0000 + c;
+          else s.con_dist[c] = (float)d64;
+        }
+        ndrop += __popcll(__ballot(drop));
+      }
+      if (lane == 0) s.kin64_mask = (unsigned long long)ndrop;   // handed to the sort (frames are dead)
+    } else if (lane == 0) {
+      s.kin64_mask = 0ull;
     }
+  } else if (lane == 0) {
+    s.kin64_mask = 0ull;
   }
   wsync();
   AW_PROF(s, PR_CO_NARROW);
@@ -1213,12 +1249,12 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
     for (int c = 0; c < NCLASS; c++) m.cls_start[c + 1] = m.cls_start[c] + ccount[c];
     if (m.npairall > JL * VS * 2) return fail(AW_EUNSUPPORTED, "too many collision pairs");
     PUT(cp_class, pcls); PUT(cp_rb, prb); PUT(cp_margin64, pmg64);
-    // per MPR pair: the bodies whose fp64 frames its geometry needs (stage_kin64), with ancestors
+    // per pair: the bodies whose fp64 frames its geometry needs (stage_kin64), with ancestors
+    // (every class: the sphere / capsule pairs' near-margin contacts are decided on fp64 frames too)
     std::vector<unsigned long long> k64(m.npairall, 0ull);
     for (int p = 0; p < m.npairall; p++)
-      if (pcls[p] == 4)
-        for (int g : {pg1[p], pg2[p]})
-          for (int b = cbody[g]; b > 0; b = parent[b]) k64[p] |= 1ull << b;
+      for (int g : {pg1[p], pg2[p]})
+        for (int b = cbody[g]; b > 0; b = parent[b]) k64[p] |= 1ull << b;
     PUT(cp_kin64, k64);
     std::vector<int> ppack(m.npairall);
     for (int p = 0; p < m.npairall; p++) ppack[p] = pcls[p] | (pg1[p] << 8) | (pg2[p] << 16);

@@ -29,11 +29,23 @@ struct Emit {
 
 AW_DEV void axis_of(float* a, const float* m, int k) { a[0] = m[k]; a[1] = m[3 + k]; a[2] = m[6 + k]; }
 
-AW_DEV void emit(Emit& e, float dist, const float* pos, const float* n) {
+// Contact activation in fp64.  Resting and grasping contacts sit AT their margin (MuJoCo's reference
+// acceleration drives dist -> margin), where fp32 geometry (~1e-7 m) decides on rounding whether a
+// contact exists -- the dominant class of teacher-forced misses in the DAPG grasp (r05c: 150 of 293
+// misses within 1e-6 of the margin, fingers / palm on the hammer handle).  So the sphere / capsule
+// colliders (classes 1, 2) emit candidates up to DEC_EPS past the margin, and every contact within
+// DEC_EPS of its margin is decided on its fp64 distance from fp64 geometry (refine_contacts64 below,
+// the frames from stage_kin64): dropped when beyond the margin, kept with the fp64 distance otherwise.
+constexpr float DEC_EPS = 2e-6f;
+
+// aux: the contact's segment parameter t (capsule - box: the sphere-box contact at axis point t),
+// kept in con_efc until the constraint rows reuse it
+AW_DEV void emit(Emit& e, float dist, const float* pos, const float* n, float aux = 0.f) {
   if (e.cnt >= MAXPAIRCON) return;
   int slot = atomicAdd(&e.s->ncon, 1);
   if (slot < MAXCON) {
     e.s->con_key[slot] = e.pair * MAXPAIRCON + e.cnt;
+    e.s->con_efc[slot] = __builtin_bit_cast(int, aux);
     e.s->con_pair[slot] = e.pair;
     e.s->con_dist[slot] = dist;
     copy3(e.s->con_pos[slot], pos);
@@ -130,7 +142,7 @@ AW_DEV void c_sphere_sphere(const float* p1, float r1, const float* p2, float r2
   sub3(dif, p2, p1);
   float cd = norm3(dif);
   float dist = cd - r1 - r2;
-  if (dist > margin) return;
+  if (dist > margin + DEC_EPS) return;   // candidates near the margin: decided in fp64
   float n[3] = {1, 0, 0};
   if (cd > MINVAL) scl3(n, dif, 1.0f / cd);
   float pos[3];
@@ -147,22 +159,25 @@ AW_DEV void c_sphere_capsule(const GV& a, const GV& b, float margin, Emit& e) {
   c_sphere_sphere(a.pos, a.size[0], q, b.size[0], margin, e);
 }
 
-AW_DEV void seg_seg(const float* p1, const float* d1, const float* p2, const float* d2, float* c1, float* c2) {
-  float r[3];
+template <class T> AW_DEV T clampt(T x, T lo, T hi) { return x < lo ? lo : (x > hi ? hi : x); }
+template <class T>
+AW_DEV void seg_seg(const T* p1, const T* d1, const T* p2, const T* d2, T* c1, T* c2) {
+  T r[3];
   sub3(r, p1, p2);
-  float a = dot3(d1, d1), ee = dot3(d2, d2), f = dot3(d2, r);
-  float s, t;
-  if (a <= MINVAL && ee <= MINVAL) { s = t = 0; }
-  else if (a <= MINVAL) { s = 0; t = clampf(f / ee, 0.f, 1.f); }
+  T a = dot3(d1, d1), ee = dot3(d2, d2), f = dot3(d2, r);
+  T s, t;
+  const T mv = T(MINVAL), z = T(0), o = T(1);
+  if (a <= mv && ee <= mv) { s = t = 0; }
+  else if (a <= mv) { s = 0; t = clampt(f / ee, z, o); }
   else {
-    float cc = dot3(d1, r);
-    if (ee <= MINVAL) { t = 0; s = clampf(-cc / a, 0.f, 1.f); }
+    T cc = dot3(d1, r);
+    if (ee <= mv) { t = 0; s = clampt(-cc / a, z, o); }
     else {
-      float b = dot3(d1, d2), den = a * ee - b * b;
-      s = den > MINVAL ? clampf((b * f - cc * ee) / den, 0.f, 1.f) : 0.f;
+      T b = dot3(d1, d2), den = a * ee - b * b;
+      s = den > mv ? clampt((b * f - cc * ee) / den, z, o) : z;
       t = (b * s + f) / ee;
-      if (t < 0) { t = 0; s = clampf(-cc / a, 0.f, 1.f); }
-      else if (t > 1) { t = 1; s = clampf((b - cc) / a, 0.f, 1.f); }
+      if (t < 0) { t = 0; s = clampt(-cc / a, z, o); }
+      else if (t > 1) { t = 1; s = clampt((b - cc) / a, z, o); }
     }
   }
   for (int k = 0; k < 3; k++) { c1[k] = p1[k] + d1[k] * s; c2[k] = p2[k] + d2[k] * t; }
@@ -176,11 +191,11 @@ AW_DEV void c_capsule_capsule(const GV& a, const GV& b, float margin, Emit& e) {
     s1[k] = a.pos[k] - a1[k] * a.size[1]; d1[k] = 2 * a1[k] * a.size[1];
     s2[k] = b.pos[k] - a2[k] * b.size[1]; d2[k] = 2 * a2[k] * b.size[1];
   }
-  seg_seg(s1, d1, s2, d2, c1, c2);
+  seg_seg<float>(s1, d1, s2, d2, c1, c2);
   c_sphere_sphere(c1, a.size[0], c2, b.size[0], margin, e);
 }
 
-AW_DEV void c_sphere_box_pt(const float* p, float r, const GV& b, float margin, Emit& e) {
+AW_DEV void c_sphere_box_pt(const float* p, float r, const GV& b, float margin, Emit& e, float t = 0.f) {
   float dif[3], loc[3], cl[3];
   sub3(dif, p, b.pos);
   mulmtv3(loc, b.mat, dif);
@@ -195,7 +210,7 @@ AW_DEV void c_sphere_box_pt(const float* p, float r, const GV& b, float margin, 
     sub3(dl, cl, loc);
     float dd = norm3(dl);
     dist = dd - r;
-    if (dist > margin) return;
+    if (dist > margin + DEC_EPS) return;   // candidates near the margin: decided in fp64
     mulmv3(dw, b.mat, dl);
     scl3(n, dw, 1.0f / dd);
   } else {
@@ -213,7 +228,7 @@ AW_DEV void c_sphere_box_pt(const float* p, float r, const GV& b, float margin, 
   }
   float pos[3];
   for (int k = 0; k < 3; k++) pos[k] = p[k] + n[k] * (r + dist / 2);
-  emit(e, dist, pos, n);
+  emit(e, dist, pos, n, t);
 }
 
 // signed distance of the box-frame point c + t u to the box of half-sizes s (< 0 inside)
@@ -364,10 +379,10 @@ AW_DEV void c_capsule_box(const GV& a, const GV& b, float margin, Emit& e, int g
   }
   float p[3];
   for (int k = 0; k < 3; k++) p[k] = a.pos[k] + ax[k] * ts;
-  c_sphere_box_pt(p, r, b, margin, e);
+  c_sphere_box_pt(p, r, b, margin, e, ts);
   if (second) {
     for (int k = 0; k < 3; k++) p[k] = a.pos[k] + ax[k] * t2;
-    c_sphere_box_pt(p, r, b, margin, e);
+    c_sphere_box_pt(p, r, b, margin, e, t2);
   }
 }
 
@@ -921,6 +936,58 @@ AW_DEV void c_convex64(const DModel& m, const mpr::GVdT<double>& own, int half, 
     for (int k = 0; k < 3; k++) { o[1 + k] = pos[k]; o[4 + k] = dir[k]; }
   }
   emit(e, (float)dist, pf, df);
+}
+
+// fp64 signed distance of contact c of a class-1 / class-2 pair (sphere / capsule pairs, sphere /
+// capsule - box) on fp64 geometry (geom64: the kin64 frames of both bodies must be staged), the same
+// construction as the fp32 collider that emitted it: sphere-sphere / sphere-capsule / capsule-capsule
+// closest points, or the sphere-box distance of the capsule axis point t the collider chose.
+AW_DEV double contact_dist64(const DModel& m, Env& s, int c) {
+  const int pair = s.con_pair[c];
+  const int g1 = MD(cp_g1, pair), g2 = MD(cp_g2, pair);
+  mpr::GVdT<double> A, B;
+  geom64(m, s, g1, A);
+  geom64(m, s, g2, B);
+  double ax[3] = {A.mat[2], A.mat[5], A.mat[8]}, p[3], q[3];
+  if (B.type != GEOM_BOX) {
+    if (A.type == GEOM_SPHERE && B.type == GEOM_SPHERE) {
+      copy3(p, A.pos);
+      copy3(q, B.pos);
+    } else if (A.type == GEOM_SPHERE) {
+      const double bx[3] = {B.mat[2], B.mat[5], B.mat[8]};
+      double dif[3];
+      sub3(dif, A.pos, B.pos);
+      const double t = clampt(dot3(dif, bx), -B.size[1], B.size[1]);
+      copy3(p, A.pos);
+      for (int k = 0; k < 3; k++) q[k] = B.pos[k] + bx[k] * t;
+    } else {
+      const double bx[3] = {B.mat[2], B.mat[5], B.mat[8]};
+      double s1[3], d1[3], s2[3], d2[3];
+      for (int k = 0; k < 3; k++) {
+        s1[k] = A.pos[k] - ax[k] * A.size[1]; d1[k] = 2 * ax[k] * A.size[1];
+        s2[k] = B.pos[k] - bx[k] * B.size[1]; d2[k] = 2 * bx[k] * B.size[1];
+      }
+      seg_seg<double>(s1, d1, s2, d2, p, q);
+    }
+    double dif[3];
+    sub3(dif, q, p);
+    return sqrt(dot3(dif, dif)) - A.size[0] - B.size[0];
+  }
+  // sphere / capsule (A) - box (B): the sphere at axis point t (0 for a sphere)
+  const double t = A.type == GEOM_CAPSULE ? (double)__builtin_bit_cast(float, s.con_efc[c]) : 0.0;
+  for (int k = 0; k < 3; k++) p[k] = A.pos[k] + ax[k] * t;
+  double dif[3], loc[3];
+  sub3(dif, p, B.pos);
+  mulmtv3(loc, B.mat, dif);
+  bool inside = true;
+  double dd = 0.0, pen = 1e300;
+  for (int k = 0; k < 3; k++) {
+    const double cl = clampt(loc[k], -B.size[k], B.size[k]);
+    if (fabs(loc[k]) > B.size[k]) inside = false;
+    dd += (cl - loc[k]) * (cl - loc[k]);
+    pen = fmin(pen, B.size[k] - fabs(loc[k]));
+  }
+  return (inside ? -pen : sqrt(dd)) - A.size[0];
 }
 
 // Conservative midphase of a sphere / capsule - box pair (class 2): false only when no point of

@@ -66,3 +66,14 @@ def test_waitlvl_calibration(tmp_path, monkeypatch):
         assert out["by_class"][c]["frac_of_wave_life"] == pytest.approx(10 * 2 * lat[c] / 4000, rel=1e-3)
     assert out["wait_any_frac"] == pytest.approx(0.4)
     assert os.path.exists(tmp_path / "profiles" / "t_waitlvl_kstep.json")
+
+
+def test_kernel_name_match_excludes_wide_tier():
+    """k_step's counters must not absorb the wide tier's drain kernel (k_step_wide launches after
+    every k_step, usually on an empty queue) or the profiling TU's variants"""
+    import summarize_profiles as sp
+    assert sp.is_kernel("void aw::fast::k_step<0>(aw::DModel, float*)", "k_step")
+    assert sp.is_kernel("k_step<2>", "k_step")
+    assert not sp.is_kernel("void aw::wide::k_step_wide<0>(aw::DModel, float*)", "k_step")
+    assert sp.is_kernel("k_step_wide<0>", "k_step_wide")
+    assert sp.is_kernel("k_random_actions(float*, int)", "k_random_actions")

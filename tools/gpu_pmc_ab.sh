@@ -13,11 +13,11 @@ for v in $2; do
   AW_LIB=$LIB timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pf_$v -o pf -- python $B3 > $OUT/pf_$v.log 2>&1
   AW_LIB=$LIB timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pw_$v -o pw -- python $B3 > $OUT/pw_$v.log 2>&1
   python - $OUT $v <<'PY'
-import csv, sys, statistics
+import csv, re, sys, statistics
 out, v = sys.argv[1], sys.argv[2]
 def ks(path, c):
     return [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if "k_step" in r["Kernel_Name"] and r["Counter_Name"] == c]
+            if re.search(r"\bk_step(?![A-Za-z0-9_])", r["Kernel_Name"]) and r["Counter_Name"] == c]
 f = ks(f"{out}/pf_{v}/pf_counter_collection.csv", "FETCH_SIZE")
 w = ks(f"{out}/pw_{v}/pw_counter_collection.csv", "WRITE_SIZE")
 n = 65536

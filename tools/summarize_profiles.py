@@ -8,6 +8,7 @@ profiles/<tag>_bench.json (the bench line of the same pass) and profiles/<tag>_p
 """
 import csv
 import json
+import re
 import os
 import shutil
 import statistics
@@ -16,10 +17,16 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def is_kernel(name, kernel):
+    """token match on the kernel name: "k_step" matches k_step<0>(...) but not k_step_wide<0>(...)
+    (the wide tier's persistent drain kernel launches after every k_step, usually on an empty queue)"""
+    return re.search(r"\b" + re.escape(kernel) + r"(?![A-Za-z0-9_])", name) is not None
+
+
 def pmc(path, counter, kernel="k_step"):
     vals, meta = [], {}
     for r in csv.DictReader(open(path)):
-        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+        if is_kernel(r["Kernel_Name"], kernel) and r["Counter_Name"] == counter:
             vals.append(float(r["Counter_Value"]))
             meta = dict(grid=int(r["Grid_Size"]), wg=int(r["Workgroup_Size"]), lds=int(r["LDS_Block_Size"]),
                         scratch=int(r["Scratch_Size"]), vgpr=int(r["VGPR_Count"]), sgpr=int(r["SGPR_Count"]),
@@ -115,7 +122,7 @@ def sq(tag):
             return None
         agg = collections.defaultdict(lambda: collections.defaultdict(float))
         for r in csv.DictReader(open(path)):
-            if "k_step" in r["Kernel_Name"]:
+            if is_kernel(r["Kernel_Name"], "k_step"):
                 agg[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
         for c, d in agg.items():
             per[c] = sum(d.values()) / len(d)
@@ -147,7 +154,7 @@ def waitlvl(tag):
     def agg(path, kern):
         a = collections.defaultdict(lambda: collections.defaultdict(float))
         for r in csv.DictReader(open(path)):
-            if kern in r["Kernel_Name"]:
+            if is_kernel(r["Kernel_Name"], kern):
                 a[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
         return {c: sum(d.values()) / len(d) for c, d in a.items()}
 
