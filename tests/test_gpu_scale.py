@@ -195,12 +195,13 @@ def test_config3_full_size_16384_envs(env_id):
 
 
 # --------------------------------------------------------------------------------------------
-# VERDICT r04's target for this regime; not met (r05b: 0.9857, every miss a classified discrete
-# event -- 150 of 293 a resting contact within 1e-6 of its margin, 126 a contact / row set that
-# differs, 3 a Newton row-state switch, 14 an fp32-unstable reference).  The gate is the floor
-# below the measurement; the target is printed beside it.
+# VERDICT r04's target for this regime.  r05b measured 0.9857 (150 of 293 misses a resting contact
+# within 1e-6 of its margin, 126 a contact / row set that differs); deciding near-margin sphere /
+# capsule contacts on fp64 frames (stage_collision) brought it to 0.9980 (r05f: 41 misses, 22 at a
+# margin, 8 a contact / row set, 11 an fp32-unstable reference), i.e. at the target to one case.
+# The gate is a floor under the measurement; the target is printed beside it.
 DAPG_HEADLINE_MIN = 0.998
-DAPG_HEADLINE_FLOOR = 0.98
+DAPG_HEADLINE_FLOOR = 0.995
 
 
 def test_dapg_teacher_forced_headline_size():

@@ -2,8 +2,13 @@
 import collections, re, subprocess, sys
 task = sys.argv[1] if len(sys.argv) > 1 else "0"   # task kind (hammer 0)
 src = "mj_envs_amd/csrc/adroit_wave.hip"
-subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-g", "-S", "--cuda-device-only", "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-fgpu-flush-denormals-to-zero",
-                f"-DAW_ONLY_TASK={task}", "-o", "/tmp/isa/one.s", src], check=True)
+import os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from __graft_entry__ import HIPCC_FLAGS  # noqa: E402  (the product build's flags)
+os.makedirs("/tmp/isa", exist_ok=True)
+flags = [f for f in HIPCC_FLAGS if f not in ("-shared", "-fPIC")]
+subprocess.run(["/opt/rocm/bin/hipcc", *flags, "-g", "-S", "--cuda-device-only",
+                f"-DAW_ONLY_TASK={task}", *sys.argv[2:], "-o", "/tmp/isa/one.s", src], check=True)
 lines = open("/tmp/isa/one.s").readlines()
 fmap = {}
 for l in lines:
