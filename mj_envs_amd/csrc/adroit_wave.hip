@@ -481,6 +481,28 @@ AW_DEV void defer_env(int* q, int env, int kind, int lane) {
 // test mode sends every forward to the wide tier)
 AW_DEV bool fast_overflow(const DModel& m, const Env& s) { return !WIDE && ((s.status & ST_OVF) != 0u || m.force_wide); }
 
+// The per-launch I/O of an env-step, parked in LDS by the launching kernel: env_step reads each
+// pointer where it is used (the substep loop's memory clobber keeps the reads there), instead of
+// ~16 SGPRs of kernel arguments -- and the per-env addresses formed from them -- held live across
+// the whole env-step, which the register allocator spilled to scratch once per env (r05h: +2 KB of
+// HBM writes per env-step).
+struct StepIO {
+  const float* actions;
+  float *obs, *reward, *terminal_obs;
+  uint8_t *done, *goal;
+  int* defer;        // fast tier: the wide-tier queue; nullptr in the wide tier
+  uint64_t seed;
+  int autoreset;
+};
+AW_DEV void park_io(StepIO& io, int lane, const float* actions, float* obs, float* reward, uint8_t* done,
+                    uint8_t* goal, float* terminal_obs, int autoreset, uint64_t seed, int* defer) {
+  if (lane == 0) {
+    io.actions = actions; io.obs = obs; io.reward = reward; io.terminal_obs = terminal_obs;
+    io.done = done; io.goal = goal; io.defer = defer; io.seed = seed; io.autoreset = autoreset;
+  }
+  wsync();
+}
+
 // One env-step of env `env`: frame_skip x (forward + Euler), task layer, and the auto-reset.
 // forward<NV> has exactly ONE inlined call site (the loop below drives substeps, the mj_checkAcc
 // retry and the reset forward through it), which keeps the code object small enough for the
@@ -489,9 +511,8 @@ AW_DEV bool fast_overflow(const DModel& m, const Env& s) { return !WIDE && ((s.s
 // reset forward, queues that forward alone).  kind DK_FORWARD (wide tier): only mj_forward + obs of
 // the stored state with ctrl 0 -- the reset forward's path through the same loop.
 template <int TASK>
-AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lane,
-                     const float* __restrict__ actions, float* obs, float* reward, uint8_t* done, uint8_t* goal,
-                     float* terminal_obs, int autoreset, uint64_t seed, int* defer, int kind = DK_STEP) {
+AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lane, const StepIO& io,
+                     int kind = DK_STEP) {
   constexpr int NV = Tree<TASK>::NV;
   wsync();
   AW_PROF_START(s);
@@ -503,14 +524,13 @@ AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lan
     if (WIDE && el == 0) s.status = ST_WIDE;
     if (el < m.nu) {
       float c = 0.f;
-      if (kind == DK_STEP) c = MD(act_mid, el) + clampf(actions[(size_t)env * m.nu + el], -1.f, 1.f) * MD(act_rng, el);
+      if (kind == DK_STEP) c = MD(act_mid, el) + clampf(io.actions[(size_t)env * m.nu + el], -1.f, 1.f) * MD(act_rng, el);
       s.ctrl[el] = c;
     }
     stage_model(m, s, st.params + (size_t)env * m.nparam, el);
   }
   float Mrow[NV];
   Dof d;
-  float* ob = obs + (size_t)env * m.obs_dim;
   int sub = 0;
   bool resetting = kind == DK_FORWARD, retry = false;
   AW_PROF(s, PR_PRE);
@@ -528,7 +548,7 @@ AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lan
     forward<TASK>(m, s, sl, Mrow, d);
     if (fast_overflow(m, s)) {
       if (!resetting) {            // nothing of this env-step is written: the wide tier re-runs it
-        defer_env(defer, env, DK_STEP, sl);
+        defer_env(io.defer, env, DK_STEP, sl);
         return;
       }
       break;                       // the reset forward alone goes to the wide tier (below)
@@ -542,18 +562,18 @@ AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lan
     if (++sub < m.frame_skip) continue;
     // env-step complete: observation, reward, episode bookkeeping
     const int tl = AW_ENV_LANE(lane);
-    write_obs(m, s, tl, ob);
+    write_obs(m, s, tl, io.obs + (size_t)env * m.obs_dim);
     int term = 0, trunc = 0;
     if (tl == 0) {
       float r;
       int dn, gl;
       task_reward(m, s, &r, &dn, &gl);
-      reward[env] = r;
-      goal[env] = (uint8_t)gl;
+      io.reward[env] = r;
+      io.goal[env] = (uint8_t)gl;
       int t = st.ep_len[env] + 1;
       term = dn;
       trunc = (m.horizon > 0 && t >= m.horizon) ? 1 : 0;
-      done[env] = (uint8_t)(term | (trunc << 1));
+      io.done[env] = (uint8_t)(term | (trunc << 1));
       float ret = st.ep_ret[env] + r;
       int gcount = st.ep_goal[env] + gl;
       st.ep_len[env] = t;
@@ -573,12 +593,12 @@ AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lan
     store_env<NV>(m, s, st, env, tl);
     AW_PROF(s, PR_TASK);
     const int ended = __builtin_amdgcn_readfirstlane(term | trunc);
-    if (!(autoreset && ended)) break;
+    if (!(io.autoreset && ended)) break;
     __threadfence_block();
-    if (terminal_obs)
-      for (int o = tl; o < m.obs_dim; o += 64) terminal_obs[(size_t)env * m.obs_dim + o] = s.rowbuf[o];
+    if (float* tob = io.terminal_obs)
+      for (int o = tl; o < m.obs_dim; o += 64) tob[(size_t)env * m.obs_dim + o] = s.rowbuf[o];
     wsync();
-    reset_prepare<NV>(m, s, st, env, tl, nullptr, seed);
+    reset_prepare<NV>(m, s, st, env, tl, nullptr, io.seed);
     if (WIDE && tl == 0) s.status |= ST_WIDE;
     AW_PROF(s, PR_RESET);
     resetting = true;
@@ -588,9 +608,9 @@ AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lan
     store_env<NV>(m, s, st, env, rl);
     if (fast_overflow(m, s)) {
       if (rl == 0) st.status_acc[env] |= s.status & ~ST_OVF;
-      defer_env(defer, env, DK_FORWARD, rl);
+      defer_env(io.defer, env, DK_FORWARD, rl);
     } else {
-      if (obs) write_obs(m, s, rl, ob);
+      if (float* ob = io.obs) write_obs(m, s, rl, ob + (size_t)env * m.obs_dim);
       if (rl == 0) {
         st.status_acc[env] |= s.status;
         if (kind == DK_FORWARD) st.status[env] |= s.status;
@@ -646,7 +666,9 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
   const DState& st = *reinterpret_cast<const DState*>(mptr + 1);   // DState follows DModel in the header
   (void)stval;
   __shared__ Env s;
+  __shared__ StepIO io;
   const int lane = threadIdx.x;
+  park_io(io, lane, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, next_env + 8);
   // Persistent workgroups: the grid is one workgroup per resident slot (launch_step); each takes
   // a first env, then the next unclaimed ones from the launch's counters, so the per-slot spill
   // block (s.slot) is rewritten in the XCD's L2 instead of streaming a per-env block to memory.
@@ -657,8 +679,7 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
   int env = xmap ? (int)((long long)n * (blockIdx.x & 7) / 8) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   if (xmap && env >= (int)((long long)n * ((blockIdx.x & 7) + 1) / 8)) env = claim_env(next_env, n, lane);
   while (env < n) {
-    env_step<TASK>(m, s, st, env, lane, actions, obs, reward, done, goal, terminal_obs, autoreset, seed,
-                   next_env + 8);
+    env_step<TASK>(m, s, st, env, lane, io);
     if ((int)gridDim.x >= n) break;            // one env per workgroup: no counter
     int claim = 0;
     if (xmap) {
@@ -738,7 +759,9 @@ __global__ void __launch_bounds__(64) k_step_wide(const DModel* __restrict__ mpt
   const DModel& m = *mptr;
   const DState& st = *reinterpret_cast<const DState*>(mptr + 1);
   __shared__ Env s;
+  __shared__ StepIO io;
   const int lane = threadIdx.x;
+  park_io(io, lane, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, nullptr);
   while (true) {
     int k = 0;
     if (lane == 0) k = atomicAdd(q + 1, 1);
@@ -752,8 +775,7 @@ __global__ void __launch_bounds__(64) k_step_wide(const DModel* __restrict__ mpt
 #ifdef AW_TRACE
     if (lane == 0) printf("wide wg %d claim %d of %d: env %d kind %d\n", (int)blockIdx.x, k, q[0], env, kind);
 #endif
-    env_step<TASK>(m, s, st, env, lane, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, nullptr,
-                   kind);
+    env_step<TASK>(m, s, st, env, lane, io, kind);
   }
 #ifdef AW_TRACE
   if (lane == 0) printf("wide wg %d: exit\n", (int)blockIdx.x);
