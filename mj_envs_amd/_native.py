@@ -131,6 +131,7 @@ def stage_profile(reset: bool = True) -> dict:
     out["offd_rows"] = v[38]
     out["co_kin64"] = v[39]
     out["cs_sparse"], out["cs_j"] = v[40], v[41]
+    out["mpr_pairs"], out["mpr_contacts"] = v[42], v[43]
     return out
 
 

@@ -256,7 +256,15 @@ AW_DEV void stage_collision(const DModel& m, Env& s, int lane) {
       wsync();
       stage_kin64(m, s, lane);
       AW_PROF(s, PR_CO_KIN64);
+#ifdef AW_STAGE_PROF
+      const int nc_before = s.ncon;
+      AW_PROF_ADD(s, PR_MPR_PAIRS, cnt[4]);
+#endif
       if (cnt[4] > 0) narrow_class<4>(m, s, plist, cnt[4], lane);
+#ifdef AW_STAGE_PROF
+      wsync();
+      AW_PROF_ADD(s, PR_MPR_CONTACTS, s.ncon - nc_before);
+#endif
       // fp64 activation: drop a candidate beyond its margin (its key moves past every valid key, so
       // the sort puts it last and cuts it), keep the others with their fp64 distance
       int ndrop = 0;
@@ -621,7 +629,7 @@ AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lan
   AW_PROF(s, PR_TASK);
   AW_PROF_COUNT(s, PR_CALLS);
   if (lane == 0)
-    for (int i = 0; i < AW_NPROF; i++) atomicAdd(&g_stage_prof[i], s.prof_acc[i]);
+    for (int i = 0; i < AW_NPROF; i++) atomicAdd(&g_stage_prof[i], (unsigned long long)s.prof_acc[i]);
 #endif
 }
 

@@ -1039,6 +1039,29 @@ AW_DEV bool mpr_may_touch(const DModel& m, const Env& s, int pair) {
     const float zero[3] = {0.f, 0.f, 0.f};
     const float circ = t1 == GEOM_CYLINDER ? sqrtf(z1[0] * z1[0] + h1 * h1) : z1[0] + h1;
     lb = seg_box_f(c, zero, s.gsize[g2], 0.f) - circ;
+#ifndef AW_NO_MPR_SAT
+    if (t1 == GEOM_CYLINDER) {
+      // separating axes: the box's three face normals and the cylinder's axis.  A gap between the
+      // two shapes' projections on a unit axis is a lower bound on their distance, and unlike the
+      // circumscribed sphere it is tight for a flat cylinder beside a face (the hammer's head over
+      // the table or the board)
+      float q1[4], m1[9], aw[3], a[3];
+      for (int k = 0; k < 4; k++) q1[k] = s.gxquat[g1][k];
+      q2m(m1, q1);
+      for (int k = 0; k < 3; k++) aw[k] = m1[3 * k + 2];
+      mulmtv3(a, mat, aw);                      // cylinder axis in the box frame
+      const float* B = s.gsize[g2];
+      float sep = -1e30f, bext = 0.f;
+      for (int k = 0; k < 3; k++) {
+        const float ak = fabsf(a[k]);
+        const float ext = ak * h1 + z1[0] * sqrtf(fmaxf(0.f, 1.f - ak * ak));   // cylinder along e_k
+        sep = fmaxf(sep, fabsf(c[k]) - B[k] - ext);
+        bext = fmaf(B[k], ak, bext);                                             // box along the axis
+      }
+      sep = fmaxf(sep, fabsf(c[0] * a[0] + c[1] * a[1] + c[2] * a[2]) - h1 - bext);
+      lb = fmaxf(lb, sep);
+    }
+#endif
   } else {
     const float* z2 = s.gsize[g2];
     const float h2 = t2 == GEOM_SPHERE ? 0.f : z2[1];

@@ -94,13 +94,14 @@ enum {
   PR_NEWTON_IT, PR_NOSLIP_IT, PR_NEFC, PR_NCON,
   PR_NT_INIT, PR_NT_HESS, PR_NT_CHOL, PR_NT_SOLVE, PR_NT_LS, PR_NT_UPD, PR_NS_MINV, PR_NS_SETUP, PR_NS_ITER,
   PR_CO_BROAD, PR_CO_NARROW, PR_COM, PR_RNE, PR_CO_C0, PR_CO_C1, PR_CO_C2, PR_CO_C3,
-  PR_NT_HSPARSE, PR_NT_HOFFD, PR_NT_OFFD_ROWS, PR_CO_KIN64, PR_CS_SPARSE, PR_CS_J
+  PR_NT_HSPARSE, PR_NT_HOFFD, PR_NT_OFFD_ROWS, PR_CO_KIN64, PR_CS_SPARSE, PR_CS_J,
+  PR_MPR_PAIRS, PR_MPR_CONTACTS   // counts: MPR pairs past the midphase, contacts they emitted
 };
-static_assert(PR_CS_J < AW_NPROF, "stage profiler ids");
+static_assert(PR_MPR_CONTACTS < AW_NPROF, "stage profiler ids");
 #ifdef AW_STAGE_PROF
 #define AW_PROF_START(S)                                            \
   do {                                                              \
-    unsigned long long _t = __builtin_amdgcn_s_memtime();           \
+    unsigned _t = (unsigned)__builtin_amdgcn_s_memtime();           \
     if (threadIdx.x == 0) {                                         \
       for (int _i = 0; _i < AW_NPROF; _i++) (S).prof_acc[_i] = 0;   \
       (S).prof_t = _t;                                              \
@@ -109,14 +110,14 @@ static_assert(PR_CS_J < AW_NPROF, "stage profiler ids");
 #define AW_PROF(S, ID)                                              \
   do {                                                              \
     __syncthreads();                                                \
-    unsigned long long _t = __builtin_amdgcn_s_memtime();           \
+    unsigned _t = (unsigned)__builtin_amdgcn_s_memtime();           \
     if (threadIdx.x == 0) {                                         \
       (S).prof_acc[ID] += _t - (S).prof_t;                          \
       (S).prof_t = _t;                                              \
     }                                                               \
   } while (0)
 #define AW_PROF_COUNT(S, ID) do { if (threadIdx.x == 0) (S).prof_acc[ID] += 1; } while (0)
-#define AW_PROF_ADD(S, ID, V) do { if (threadIdx.x == 0) (S).prof_acc[ID] += (unsigned long long)(V); } while (0)
+#define AW_PROF_ADD(S, ID, V) do { if (threadIdx.x == 0) (S).prof_acc[ID] += (unsigned)(V); } while (0)
 #elif defined(AW_TRACE)   // debugging builds: every stage boundary printed by lane 0 (device printf)
 #define AW_PROF_START(S) ((void)0)
 #define AW_PROF(S, ID) do { if (threadIdx.x == 0) printf("wg %d stage %d\n", (int)blockIdx.x, (int)(ID)); } while (0)
@@ -320,8 +321,10 @@ struct __attribute__((aligned(16))) Env {
                               // reused by every env the persistent k_step workgroup processes
   int it_newton, it_noslip;   // iterations of the last solve (introspection)
 #ifdef AW_STAGE_PROF
-  unsigned long long prof_acc[AW_NPROF];
-  unsigned long long prof_t;
+  // 32-bit: one env-step's cycles per stage (summed into 64-bit globals after each env-step); keeps
+  // the profiling build's Env inside k_step's 20 480-byte LDS granule, i.e. at the product's occupancy
+  unsigned prof_acc[AW_NPROF];
+  unsigned prof_t;
 #endif
 };
 

@@ -96,7 +96,8 @@ def main():
                avg_newton_iters_per_solve=round(p["newton_iters"] / sub, 3),
                avg_noslip_iters_per_substep=round(p["noslip_iters"] / sub, 3),
                avg_nefc=round(p["nefc"] / sub, 3), avg_ncon=round(p["ncon"] / sub, 3),
-               avg_offd_rows=round(p["offd_rows"] / sub, 3))
+               avg_offd_rows=round(p["offd_rows"] / sub, 3),
+               avg_mpr_pairs=round(p["mpr_pairs"] / sub, 4), avg_mpr_contacts=round(p["mpr_contacts"] / sub, 4))
     txt = json.dumps(res, indent=1)
     print(txt)
     if a.out:
