@@ -1513,6 +1513,17 @@ static int check_tree(const Blob& B, int task_kind) {
   return AW_OK;
 }
 
+// the fast tier's dense-row capacity of the handle's task: per task in the split build (each task's
+// translation unit compiles its own, aw_common.h), the single value of a one-TU diagnostic build
+static int fast_maxdense_handle(const aw_handle* h) {
+#ifdef AW_API_TU
+  return fast_maxdense_of(h->m.task_kind);
+#else
+  (void)h;
+  return FAST_MAXDENSE;
+#endif
+}
+
 // persistent grid of the k_step instantiation the handle currently selects
 static int update_slots(aw_handle* h) {
   if (h->grid_env >= 0) {
@@ -1611,7 +1622,7 @@ int aw_dims(const aw_handle* h, int* d) {
   const DModel& m = h->m;
   int v[AW_NDIMS] = {m.nq, m.nv, m.nu, m.obs_dim, m.nparam, m.frame_skip, m.horizon, m.task_kind, h->nenv,
                      m.nbody, m.nsite, m.ngeom, m.npairall, NCONMAX, NJMAX, WIDE_MAXDENSE, std::min(h->slots, h->nenv),
-                     FAST_MAXCON, 64 * FAST_NRL, FAST_MAXDENSE, h->wide_grid};
+                     FAST_MAXCON, 64 * FAST_NRL, fast_maxdense_handle(h), h->wide_grid};
   memcpy(d, v, sizeof(v));
   return AW_OK;
 }

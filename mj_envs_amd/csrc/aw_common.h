@@ -47,7 +47,23 @@ constexpr int NCLASS = 5;      // collider classes: plane-*, round-round, round-
 // a per-tier inline namespace, so the two translation units that instantiate the same functions
 // with different capacities never share a (mangled) name.
 namespace aw {
-constexpr int FAST_MAXCON = 48, FAST_NRL = 3, FAST_MAXDENSE = 128;
+// Fast-tier dense-row capacity per task: 128 (the DAPG regimes peak at 98, random hammer at 37);
+// relocate's random-action tail -- the hand cupping the ball, 25-30 pyramidal contacts -- reaches
+// 126-140 dense rows, so relocate's fast tier holds 192 (its whole row capacity) and the wide tier
+// sees 2 instead of 10 of 16 384 envs per 200 steps: config 3 relocate -4.4 %, hammer unchanged
+// (r05q A/B).  The host allocates the spill blocks for the largest value.
+constexpr int fast_maxdense_of(int task) { return task == 3 ? 192 : 128; }
+constexpr int FAST_MAXDENSE_ALLOC = 192;
+#if defined(AW_FAST_MAXDENSE)
+#elif defined(AW_TASK_TU)
+#define AW_FAST_MAXDENSE fast_maxdense_of(AW_TASK_TU)
+#elif defined(AW_ONLY_TASK)
+#define AW_FAST_MAXDENSE fast_maxdense_of(AW_ONLY_TASK)
+#else
+#define AW_FAST_MAXDENSE 128   // single-TU builds of all four tasks (diagnostics): one Env for all
+#endif
+constexpr int FAST_MAXCON = 48, FAST_NRL = 3, FAST_MAXDENSE = AW_FAST_MAXDENSE;
+static_assert(FAST_MAXDENSE <= FAST_MAXDENSE_ALLOC, "fast spill blocks are allocated for FAST_MAXDENSE_ALLOC");
 constexpr int WIDE_MAXCON = 100, WIDE_NRL = 8, WIDE_MAXDENSE = 500;
 constexpr int NCONMAX = 100, NJMAX = 500;   // the reference model's caps (DAPG_assets.xml:4)
 #ifdef AW_WIDE
@@ -76,7 +92,7 @@ static_assert(EFC_CAP <= MAXEFC && MAXDENSE <= EFC_CAP, "constraint capacities")
 }  // namespace aw
 
 namespace aw {
-constexpr int JSPILL_FAST = (FAST_MAXDENSE - 32) * VS, JSPILL_WIDE = (WIDE_MAXDENSE - 32) * VS;
+constexpr int JSPILL_FAST = (FAST_MAXDENSE_ALLOC - 32) * VS, JSPILL_WIDE = (WIDE_MAXDENSE - 32) * VS;
 #ifdef AW_WIDE
 #define AW_TIER wide
 #else

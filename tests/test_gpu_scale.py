@@ -133,6 +133,8 @@ def test_config3_full_size_16384_envs(env_id):
     _, sim = _sim(env_id, n)
     assert sim.grid < n, f"grid {sim.grid} covers all {n} envs: the persistent claim path is not exercised"
     assert (sim.maxcon, sim.maxefc) == (100, 500), "effective capacities must be MuJoCo's nconmax / njmax"
+    # the fast tier's dense rows: relocate's own TU holds 192 (aw_common.h fast_maxdense_of)
+    assert sim.fast_maxdense == (192 if env_id == "relocate-v0" else 128), sim.fast_maxdense
     obs, rew, done, goal = _bufs(sim, n)
     sim.reset(obs, seed=7)
     sim.set_episode(ep_len=torch.from_numpy((np.arange(n) * 7919 % sim.horizon).astype(np.int32)).cuda())
