@@ -58,7 +58,8 @@ enum {
  * constraint rows and dense (contact) rows -- the reference model's own, nconmax 100 / njmax 500
  * (DAPG_assets.xml:4); a step that needs more drops what MuJoCo drops and raises
  * AW_ST_*_OVERFLOW.  Two tiers hold them: every env-step runs in the fast tier (FAST_* capacities,
- * two waves per SIMD); one that needs more is abandoned there before anything is written and
+ * per task -- FAST_MAXDENSE is 192 for relocate-v0, 128 for the others -- two waves per SIMD); one
+ * that needs more is abandoned there before anything is written and
  * re-run in the same aw_step / aw_reset / aw_set_state call by the wide tier (MuJoCo's
  * capacities, WIDE_GRID persistent workgroups), which marks it AW_ST_WIDE.
  * GRID: workgroups of one aw_step launch (one per resident slot on the device, capped at
