@@ -6,6 +6,7 @@
 // mj_fwdActuation (see oracle/mjstep.cc for the fp64 statement of the same stages).
 #pragma once
 #include "aw_common.h"
+#include "aw_sincos64.h"
 
 namespace aw {
 
@@ -203,41 +204,17 @@ AW_DEV void apply_ovr64(const DModel& m, const Env& s, int field, int obj, doubl
     }
 }
 
-// sin / cos of a joint half-angle in fp64: one-pass Cody-Waite reduction by pi/2 (a 33-bit head and
-// its tail, carried as a double-double into the kernels) and the classic minimax kernels of fdlibm's
-// k_sin / k_cos (published coefficients).  Host-checked against libm over fp32 joint angles and
-// |x| < 1e5 (build/sc: <= 1 ulp with contraction, as compiled here).  It replaces ocml's sincos,
-// whose table-driven large-argument path left eight 64-bit table addresses hoisted out of the env
-// loop and reloaded from scratch on every call.
-// The reduction and kernel constants live in constant memory and are read where they are used
-// through a pointer the compiler cannot see through: as literals, LICM hoisted them out of the env
-// loop into nine VGPR pairs that the allocator then reloaded from scratch on every call.
-static __constant__ double SINCOS64_K[15] = {
-    6.36619772367581382433e-01,                                 // 2 / pi
-    1.57079632673412561417e+00, 6.07710050650619224932e-11,     // pi / 2: 33-bit head, tail
-    -1.66666666666666324348e-01, 8.33333333332248946124e-03, -1.98412698298579493134e-04,
-    2.75573137070700676789e-06, -2.50507602534068634195e-08, 1.58969099521155010221e-10,   // S1..S6
-    4.16666666666666019037e-02, -1.38888888888741095749e-03, 2.48015872894767294178e-05,
-    -2.75573143513906633035e-07, 2.08757232129817482790e-09, -1.13596475577881948265e-11};  // C1..C6
+// sin / cos of a joint half-angle in fp64 (aw_sincos64.h, shared with the host check
+// tests/sincos64_check.cc).  It replaces ocml's sincos, whose table-driven large-argument path left
+// 64-bit table addresses hoisted out of the env loop and reloaded from scratch on every call; the
+// constants live in constant memory and are read where they are used through a pointer the
+// compiler cannot see through (as literals, LICM hoisted them into nine VGPR pairs that the
+// allocator reloaded from scratch on every call as well).
+static __constant__ double SINCOS64_K[15] = AW_SINCOS64_K;
 AW_DEV void sincos64(double x, double* sn, double* cs) {
   const double* K = SINCOS64_K;
   asm volatile("" : "+s"(K));
-  const double fn = rint(x * K[0]);
-  const double r = x - fn * K[1], w = fn * K[2];
-  const double y0 = r - w, y1 = (r - y0) - w;
-  const double z = y0 * y0;
-  const double v = z * y0, rs = K[4] + z * (K[5] + z * (K[6] + z * (K[7] + z * K[8])));
-  const double ks = y0 - ((z * (0.5 * y1 - v * rs) - y1) - v * K[3]);
-  const double rc = z * (K[9] + z * (K[10] + z * (K[11] + z * (K[12] + z * (K[13] + z * K[14])))));
-  const double ay = fabs(y0);
-  // |y0| >= 0.3: cos = (1 - qx) - ((z/2 - qx) - ...), qx = |y0| / 4 with the low word cleared
-  // (0.28125 past 0.78125), which keeps 1 - qx exact
-  const double qx = ay < 0.3 ? 0.0 : ay > 0.78125 ? 0.28125
-                  : __longlong_as_double((__double_as_longlong(ay) - (0x00200000ll << 32)) & ~0xffffffffll);
-  const double kc = (1.0 - qx) - ((0.5 * z - qx) - (z * rc - y0 * y1));
-  const int n = (int)(long long)fn & 3;
-  *sn = n == 0 ? ks : n == 1 ? kc : n == 2 ? -ks : -kc;
-  *cs = n == 0 ? kc : n == 1 ? -ks : n == 2 ? -kc : ks;
+  sincos64_k(x, K, sn, cs);
 }
 
 // mj_kinematics in fp64 for the bodies that carry the geometry of this substep's MPR (cylinder)
