@@ -25,10 +25,21 @@ def oracle_lib():
     return pyoracle
 
 
-def make_oracle(env_id, variation_type=None):
+def load_task_model(env_id, variation_type=None):
+    """The task model as the tests build it: the reference's variation types, plus the test-only
+    pseudo-variation "margin=X" (every geom margin set to X: far more contacts and rows than the
+    reference's regimes, to drive the wide capacity tier)"""
     from mj_envs_amd.tasks import attach_task, load_model
+    if variation_type and str(variation_type).startswith("margin="):
+        m = attach_task(load_model(env_id), env_id, None)
+        m.arrays["geom_margin"] = np.full_like(m.arrays["geom_margin"], float(variation_type.split("=")[1]))
+        return m
+    return attach_task(load_model(env_id), env_id, variation_type)
+
+
+def make_oracle(env_id, variation_type=None):
     from oracle.pyoracle import Oracle
-    m = attach_task(load_model(env_id), env_id, variation_type)
+    m = load_task_model(env_id, variation_type)
     return m, Oracle(m.to_blob())
 
 

@@ -12,7 +12,7 @@ Tolerances (stated per the north star's "fp32 tolerance"):
 import numpy as np
 import pytest
 
-from conftest import ENVS, golden, make_oracle
+from conftest import ENVS, golden, load_task_model, make_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -25,8 +25,7 @@ def _t(a, dtype=None):
 
 def _sim(env_id, n, variation=None):
     from mj_envs_amd import _native
-    from mj_envs_amd.tasks import attach_task, load_model
-    m = attach_task(load_model(env_id), env_id, variation)
+    m = load_task_model(env_id, variation)
     return m, _native.Sim(m.to_blob(), n)
 
 
@@ -122,6 +121,11 @@ def _discrete_at(m, o, one, params, q, v, w, ctrl, tol=1e-6):
     c = o.get("contact").reshape(-1, 23)
     one.set_state(_t(q[None]), _t(v[None]), _t(w[None]), _t(np.asarray(params)[None]))
     d = one.forward_dump(0, _t(ctrl))
+    from mj_envs_amd import _native
+    if int(d["status"]) & _native.ST_OVERFLOW:
+        # the dump runs the fast tier: past its capacities its contact / row lists are truncated and
+        # say nothing about the wide tier's -- no discrete event can be established from it
+        return None
     if d["ncon"] != int(sc[0]) or d["nefc"] != int(sc[1]):
         return f"contact / row set (ncon {d['ncon']} vs {int(sc[0])}, nefc {d['nefc']} vs {int(sc[1])})"
     if len(c) and np.min(np.abs(c[:, 0] - c[:, 17])) < tol:
@@ -147,9 +151,8 @@ def _discrete_event(env_id, variation, o, params, qpos, qvel, warm, act, frame_s
     satisfied on the other, a frictionloss row sticking on one side and sliding on the other: the
     stick-slip switch of mj_solNewton's piecewise-quadratic cost).  `why` (a list) receives the
     reason."""
-    from mj_envs_amd.tasks import attach_task, load_model
     from mj_envs_amd import _native
-    m = attach_task(load_model(env_id), env_id, variation)
+    m = load_task_model(env_id, variation)
     one = _native.Sim(m.to_blob(), 1)
     ctrl = m.task_act_mid + np.clip(act, -1, 1) * m.task_act_rng
     q, v, w = qpos.copy(), qvel.copy(), warm.copy()
@@ -207,9 +210,8 @@ def _oracle_f32_model(env_id, variation=None):
     fp32 (the kernel's model table is fp32)."""
     key = (env_id, variation)
     if key not in _ORACLE_F32MODEL:
-        from mj_envs_amd.tasks import attach_task, load_model
         from oracle.pyoracle import Oracle
-        m = attach_task(load_model(env_id), env_id, variation)
+        m = load_task_model(env_id, variation)
         for k, v in list(m.arrays.items()):
             a = np.asarray(v)
             if a.dtype.kind == "f":
@@ -308,11 +310,10 @@ def _shadowed_trajectory(env_id, variation, o1, params, qpos, qvel, warm, act, f
     substep from that state, and the replay ends on the GPU's env-step result (gpu = (qpos, qvel));
     "discrete" when a substep is not, but the two sides' forwards at that GPU state differ by a
     discrete event (_discrete_at); None otherwise."""
-    from mj_envs_amd.tasks import attach_task, load_model
     from mj_envs_amd import _native
     if gpu is None:
         return False
-    m = attach_task(load_model(env_id), env_id, variation)
+    m = load_task_model(env_id, variation)
     m.dims["task_frame_skip"] = 1
     one = _native.Sim(m.to_blob(), 1)
     ob, rw = one.empty(1, one.obs_dim), one.empty(1)

@@ -264,3 +264,4 @@ def test_dapg_teacher_forced_headline_size():
     assert not unexplained, unexplained
     _err_gate(err)
     print(f"{label}: DAPG_HEADLINE_MIN target {DAPG_HEADLINE_MIN}: {'met' if frac >= DAPG_HEADLINE_MIN else 'NOT met'}")
+
