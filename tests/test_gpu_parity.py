@@ -352,10 +352,11 @@ def _shadowed_trajectory(env_id, variation, o1, params, qpos, qvel, warm, act, f
 
 def _classify_misses(env_id, misses, frame_skip, variation=None):
     """every miss must be a discrete event (_discrete_event: the contact / row set differs, or a
-    contact sits within fp32 rounding of its margin), a step the fp64 reference itself cannot
-    resolve at fp32 resolution with the GPU inside that spread (_fp32_sensitive), or a GPU
-    trajectory the oracle shadows substep by substep from the GPU's own states (_shadowed_trajectory):
-    returns the unexplained ones.  A miss is (step, env, params, qpos, qvel, warm, action[, gpu_qpos, gpu_qvel])."""
+    contact sits within fp32 rounding of its margin), a GPU trajectory the oracle shadows substep by
+    substep from the GPU's own states or that meets such an event on its own trajectory
+    (_shadowed_trajectory), or a step the fp64 reference itself cannot resolve at fp32 resolution
+    with the GPU inside that spread (_fp32_sensitive) -- tried in that order, the strongest evidence
+    first: returns the unexplained ones.  A miss is (step, env, params, qpos, qvel, warm, action[, gpu_qpos, gpu_qvel])."""
     if not misses:
         return []
     o = make_oracle(env_id, variation)[1]
@@ -370,15 +371,17 @@ def _classify_misses(env_id, misses, frame_skip, variation=None):
                 key = "contact / row set"
             kinds[key] = kinds.get(key, 0) + 1
             continue
-        if _fp32_sensitive(o, params, q, v, w, a, env_id, variation, gpu=gpu):
-            kinds["fp32-sensitive reference"] = kinds.get("fp32-sensitive reference", 0) + 1
-            continue
+        # the stronger evidence first: the GPU's own trajectory checked substep by substep against
+        # the oracle (a switch on it, or every substep locally right), then the reference's spread
         why = []
         sh = _shadowed_trajectory(env_id, variation, o, params, q, v, w, a, frame_skip, gpu, why=why)
         if sh is not None:
             key = "oracle-shadowed trajectory" if sh == "shadowed" else "discrete event on the GPU's own trajectory"
             kinds[key] = kinds.get(key, 0) + 1
             print(f"  step {k} env {e}: {why[-1]}")
+            continue
+        if _fp32_sensitive(o, params, q, v, w, a, env_id, variation, gpu=gpu):
+            kinds["fp32-sensitive reference"] = kinds.get("fp32-sensitive reference", 0) + 1
             continue
         print(f"  unexplained step {k} env {e}: {why}")
         out.append((k, e))
