@@ -501,12 +501,16 @@ struct StepIO {
   int* defer;        // fast tier: the wide-tier queue; nullptr in the wide tier
   uint64_t seed;
   int autoreset;
+  unsigned* cost;    // per env: shader cycles of its last env-step (k_order's sort key); nullptr: off
+  const int* perm;   // claim position -> env (k_order: each XCD class's envs, most expensive first)
+  unsigned long long t0;   // this workgroup's current env-step start (s_memtime)
 };
 AW_DEV void park_io(StepIO& io, int lane, const float* actions, float* obs, float* reward, uint8_t* done,
                     uint8_t* goal, float* terminal_obs, int autoreset, uint64_t seed, int* defer) {
   if (lane == 0) {
     io.actions = actions; io.obs = obs; io.reward = reward; io.terminal_obs = terminal_obs;
     io.done = done; io.goal = goal; io.defer = defer; io.seed = seed; io.autoreset = autoreset;
+    io.cost = nullptr; io.perm = nullptr; io.t0 = 0;
   }
   wsync();
 }
@@ -519,11 +523,12 @@ AW_DEV void park_io(StepIO& io, int lane, const float* actions, float* obs, floa
 // reset forward, queues that forward alone).  kind DK_FORWARD (wide tier): only mj_forward + obs of
 // the stored state with ctrl 0 -- the reset forward's path through the same loop.
 template <int TASK>
-AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lane, const StepIO& io,
+AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lane, StepIO& io,
                      int kind = DK_STEP) {
   constexpr int NV = Tree<TASK>::NV;
   wsync();
   AW_PROF_START(s);
+  if (lane == 0 && io.cost) io.t0 = __builtin_amdgcn_s_memtime();
   {
     // an opaque lane id here and in the env-step tail below: per-lane state / obs addresses
     // are formed where they are used instead of once per env and spilled to scratch
@@ -625,6 +630,11 @@ AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lan
       }
     }
   }
+  // this env-step's cost for the next launch's claim order (k_order)
+  if (lane == 0 && io.cost) {
+    const unsigned long long dt = __builtin_amdgcn_s_memtime() - io.t0;
+    io.cost[env] = dt > 0xffffffffull ? 0xffffffffu : (unsigned)dt;
+  }
 #ifdef AW_STAGE_PROF
   AW_PROF(s, PR_TASK);
   AW_PROF_COUNT(s, PR_CALLS);
@@ -677,17 +687,29 @@ __global__ void __launch_bounds__(64) AW_KSTEP_ATTR k_step(DModel mval, const DM
   __shared__ StepIO io;
   const int lane = threadIdx.x;
   park_io(io, lane, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, next_env + 8);
+  const bool xmap = (int)gridDim.x < n && (gridDim.x & 7) == 0;
+  // claim positions map to envs through k_order's permutation (same XCD class, costliest first:
+  // the launch's last claims are its cheapest envs, r05 A/B -0.3 % random, -2.9 % DAPG)
+  if (lane == 0) {
+    io.cost = xmap ? reinterpret_cast<unsigned*>(next_env + 10 + n) : nullptr;
+    io.perm = xmap ? next_env + 10 + 2 * n : nullptr;
+  }
+  wsync();
+  auto env_of = [&](int pos) {
+    if (!io.perm) return pos;
+    const int e = io.perm[pos];
+    return (unsigned)e < (unsigned)n ? e : pos;
+  };
   // Persistent workgroups: the grid is one workgroup per resident slot (launch_step); each takes
   // a first env, then the next unclaimed ones from the launch's counters, so the per-slot spill
   // block (s.slot) is rewritten in the XCD's L2 instead of streaming a per-env block to memory.
   // Envs go out in XCD-contiguous ranges (claim_env above); grids that are not a multiple of 8
   // workgroups (AW_STEP_GRID) take env blockIdx.x first and then claim from one counter.  Every
   // workgroup exits once the counters pass n.
-  const bool xmap = (int)gridDim.x < n && (gridDim.x & 7) == 0;
   int env = xmap ? (int)((long long)n * (blockIdx.x & 7) / 8) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   if (xmap && env >= (int)((long long)n * ((blockIdx.x & 7) + 1) / 8)) env = claim_env(next_env, n, lane);
   while (env < n) {
-    env_step<TASK>(m, s, st, env, lane, io);
+    env_step<TASK>(m, s, st, env_of(env), lane, io);
     if ((int)gridDim.x >= n) break;            // one env per workgroup: no counter
     int claim = 0;
     if (xmap) {
@@ -1034,7 +1056,9 @@ struct aw_handle {
   void* dmhdr = nullptr;   // device copy of m (k_step reads its scalars from here)
   void* dstate = nullptr;
   int* next_env = nullptr;   // [0, 8): k_step's per-XCD claim counters; [8, 10 + nenv): the wide-tier
-                             // queue (count, claim counter, entries; adroit_wave.hip defer_env)
+                             // queue (count, claim counter, entries; adroit_wave.hip defer_env);
+                             // [10 + nenv, 10 + 2 nenv): per-env env-step cycles, [10 + 2 nenv,
+                             // 10 + 3 nenv): the claim permutation (k_order)
   int slots = 0;             // persistent k_step grid: resident workgroups of the selected instantiation,
                              // or AW_STEP_GRID (read at aw_create; 0 = one workgroup per env)
   int grid_env = -1;         // AW_STEP_GRID at create (-1: unset)
@@ -1405,6 +1429,36 @@ static int step_slots(int device) {
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
   return std::max(per_cu, 1) * std::max(cus, 1);
 }
+// Claim order for the next k_step launch (longest processing time first): per XCD class c (k_step's
+// env range [n c / 8, n (c + 1) / 8)) the envs are bucketed by their last env-step's shader cycles
+// on a quarter-octave scale and written costliest bucket first into perm (positions of the same
+// range), so the launch's last claims are its cheapest envs.  One workgroup per class.
+static __device__ int cost_bucket(unsigned c) {
+  if (c < (1u << 16)) return 0;
+  const int e = 31 - __clz(c);                       // floor(log2 c) >= 16
+  const int key = 4 * e + (int)((c >> (e - 2)) & 3);  // quarter octaves
+  const int b = key - 4 * 16;
+  return b > 63 ? 63 : b;
+}
+static __global__ void __launch_bounds__(1024) k_order(const unsigned* __restrict__ cost, int* __restrict__ perm, int n) {
+  const int c = blockIdx.x;
+  const int lo = (int)((long long)n * c / 8), hi = (int)((long long)n * (c + 1) / 8);
+  __shared__ int hist[64];
+  if (threadIdx.x < 64) hist[threadIdx.x] = 0;
+  __syncthreads();
+  for (int i = lo + (int)threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&hist[cost_bucket(cost[i])], 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int b = 63; b >= 0; b--) { const int h = hist[b]; hist[b] = acc; acc += h; }
+  }
+  __syncthreads();
+  for (int i = lo + (int)threadIdx.x; i < hi; i += blockDim.x) {
+    const int k = atomicAdd(&hist[cost_bucket(cost[i])], 1);
+    perm[lo + k] = i;
+  }
+}
+
 // every launch that runs a fast-tier forward clears the wide queue first and drains it after
 static void clear_queue(aw_handle* h, bool counters, hipStream_t st) {
   if (counters) (void)hipMemsetAsync(h->next_env, 0, 10 * sizeof(int), st);   // XCD counters + queue heads
@@ -1416,6 +1470,9 @@ static void launch_step(aw_handle* h, const float* a, float* obs, float* rew, ui
   // grid = the handle's persistent slot count (aw_create / aw_set_option), capped at nenv
   const int grid = std::min(h->nenv, h->slots);
   clear_queue(h, grid < h->nenv, st);
+  if (grid < h->nenv && (grid & 7) == 0)   // the XCD-class claim path (k_step xmap)
+    hipLaunchKernelGGL(k_order, dim3(8), dim3(1024), 0, st, reinterpret_cast<const unsigned*>(h->next_env + 10 + h->nenv),
+                       h->next_env + 10 + 2 * h->nenv, h->nenv);
   hipLaunchKernelGGL((k_step<TASK>), dim3(grid), dim3(64), 0, st, h->m, (const DModel*)h->dmhdr, h->st, h->nenv, a, obs, rew, done,
                      goal, tobs, autoreset, seed, h->next_env);
   wide_ops<TASK>()->run(h, a, obs, rew, done, goal, tobs, autoreset, seed, st);
@@ -1584,8 +1641,9 @@ int aw_create(const void* blob, size_t nbytes, int n_envs, int device, aw_handle
   // fast tier: one spill block per workgroup of k_reset / k_set_state (one per env)
   HIPCHK(hipMalloc((void**)&h->m.jspill, (size_t)n_envs * JSPILL_FAST * sizeof(float)));
   HIPCHK(hipMalloc(&h->dmhdr, sizeof(DModel) + sizeof(DState)));
-  HIPCHK(hipMalloc((void**)&h->next_env, (10 + (size_t)n_envs) * sizeof(int)));
-  HIPCHK(hipMemset(h->next_env, 0, (10 + (size_t)n_envs) * sizeof(int)));
+  const size_t nq = 10 + 3 * (size_t)n_envs;   // + per-env costs and the claim permutation (k_order)
+  HIPCHK(hipMalloc((void**)&h->next_env, nq * sizeof(int)));
+  HIPCHK(hipMemset(h->next_env, 0, nq * sizeof(int)));
   // wide tier: its persistent grid and one spill block per wide workgroup
 #define CALL(TT) (h->wide_grid = std::min(n_envs, wide_ops<TT>()->slots(device)))
   DISPATCH_TASK(h->m.task_kind, CALL)
