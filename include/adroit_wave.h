@@ -64,7 +64,8 @@ enum {
  * capacities, WIDE_GRID persistent workgroups), which marks it AW_ST_WIDE.
  * GRID: workgroups of one aw_step launch (one per resident slot on the device, capped at
  * n_envs); below n_envs the persistent workgroups claim the remaining envs from per-XCD
- * counters (contiguous env ranges per XCD, stealing once a range is exhausted). */
+ * counters (contiguous env ranges per XCD, stealing once a range is exhausted), each range in
+ * descending order of its envs' last env-step cost (longest processing time first). */
 enum {
   AW_DIM_NQ, AW_DIM_NV, AW_DIM_NU, AW_DIM_OBS, AW_DIM_NPARAM, AW_DIM_FRAME_SKIP,
   AW_DIM_HORIZON, AW_DIM_TASK, AW_DIM_NENV, AW_DIM_NBODY, AW_DIM_NSITE, AW_DIM_NGEOM,
