@@ -12,7 +12,8 @@
   against the fp64 oracle (relocate_v0.py:85-93 resets, *_v0.py step).
 * The DAPG regime at the headline size (hammer-v0, 65 536 envs, the reference's pretrained
   policy, mean actions as algos/baselines.py:82-86): 256 envs sampled across the batch are
-  teacher-forced through the hammer strike (hammer_v0.py:54-90).
+  teacher-forced through the hammer strike (hammer_v0.py:54-90); door / pen / relocate in their
+  DAPG regimes at config 3's size (16 384 envs) the same way.
 """
 import os
 
@@ -206,19 +207,18 @@ DAPG_HEADLINE_MIN = 0.998
 DAPG_HEADLINE_FLOOR = 0.995
 
 
-def test_dapg_teacher_forced_headline_size():
-    """hammer-v0, 65 536 envs in the DAPG closed loop (k_mlp mean actions): 256 envs sampled across
-    the batch teacher-forced over env-steps 40..119 (grasp, lift, the strike on the nail)."""
-    from mj_envs_amd import _native
+def _dapg_teacher_forced(env_id, n, warm_steps, steps, seed):
+    """n envs in the DAPG closed loop (k_mlp mean actions) after warm_steps env-steps; 256 envs
+    sampled across the batch teacher-forced over the next `steps` env-steps.  Returns (label, frac,
+    reward frac, error report, unexplained misses, sticky status)."""
     from mj_envs_amd.policy import GaussianMLP
-    env_id, n, warm_steps, steps = "hammer-v0", 65536, 40, 80
     m, o = make_oracle(env_id)
     _, sim = _sim(env_id, n)
     assert sim.grid < n
-    pol = GaussianMLP.from_npz(os.path.join(GOLDEN, "dapg_hammer.npz"), device=0)
+    pol = GaussianMLP.from_npz(os.path.join(GOLDEN, f"dapg_{env_id.split('-')[0]}.npz"), device=0)
     obs, rew, done, goal = _bufs(sim, n)
     act = sim.empty(n, sim.nu)
-    sim.reset(obs, seed=31)
+    sim.reset(obs, seed=seed)
     for k in range(warm_steps):
         pol.act(obs, out=act)
         sim.step(act, obs, rew, done, goal)
@@ -249,19 +249,42 @@ def test_dapg_teacher_forced_headline_size():
                     a[j], qg[j].astype(np.float64), vg[j].astype(np.float64)) for j in np.where(~okk)[0]]
         roks.append(_rewards_close(rew.cpu().numpy()[idx], r_ref, check=False))
         if k % 20 == 0:
-            print(f"  DAPG step {warm_steps + k}: {len(misses)} misses so far", flush=True)
+            print(f"  {env_id} DAPG step {warm_steps + k}: {len(misses)} misses so far", flush=True)
     ok = np.concatenate(oks)
     frac, rfrac = ok.mean(), np.concatenate(roks).mean()
-    label = f"DAPG headline size (hammer-v0, {n} envs, grid {sim.grid})"
+    label = f"DAPG {env_id} ({n} envs, grid {sim.grid})"
     print(f"{label}: {frac:.4f} of {ok.size} sampled (env, step) cases within tolerance, rewards {rfrac:.4f}")
     err = _err_report(label, np.concatenate(eqs), np.concatenate(evs), ok)
     _hard_cap(np.concatenate(eqs), np.concatenate(evs), label)
     unexplained = _classify_misses(env_id, misses, sim.frame_skip)
     print(f"{label}: {len(misses)} misses at steps {sorted(set(ms[0] for ms in misses))}, unexplained: {unexplained}")
     _, sticky = _status(sim, n)
+    return label, frac, rfrac, err, unexplained, sticky
+
+
+def test_dapg_teacher_forced_headline_size():
+    """hammer-v0, 65 536 envs in the DAPG closed loop (k_mlp mean actions): 256 envs sampled across
+    the batch teacher-forced over env-steps 40..119 (grasp, lift, the strike on the nail)."""
+    from mj_envs_amd import _native
+    label, frac, rfrac, err, unexplained, sticky = _dapg_teacher_forced("hammer-v0", 65536, 40, 80, 31)
     assert not ((sticky & _native.ST_OVERFLOW) != 0).any()
     assert frac >= DAPG_HEADLINE_FLOOR and rfrac >= REWARD_MIN, (frac, rfrac)
     assert not unexplained, unexplained
     _err_gate(err)
     print(f"{label}: DAPG_HEADLINE_MIN target {DAPG_HEADLINE_MIN}: {'met' if frac >= DAPG_HEADLINE_MIN else 'NOT met'}")
+
+
+# door / pen / relocate in their DAPG grasp regimes at BASELINE config 3's size (16 384 envs,
+# persistent claims), env-steps 20..79 (pen's horizon is 100)
+DAPG_C3_FLOOR = 0.995   # r05zd: door 1.0000, pen 0.9995, relocate 0.9999
+
+
+@pytest.mark.parametrize("env_id", ["door-v0", "pen-v0", "relocate-v0"])
+def test_dapg_teacher_forced_config3_size(env_id):
+    from mj_envs_amd import _native
+    label, frac, rfrac, err, unexplained, sticky = _dapg_teacher_forced(env_id, 16384, 20, 60, 37)
+    assert not ((sticky & _native.ST_OVERFLOW) != 0).any()
+    assert frac >= DAPG_C3_FLOOR and rfrac >= REWARD_MIN, (frac, rfrac)
+    assert not unexplained, unexplained
+    _err_gate(err)
 
