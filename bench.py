@@ -290,14 +290,24 @@ def dry_run(args, shard):
         dist.destroy_process_group()
 
 
+def default_preroll(horizon, warmup, steps):
+    """untimed pre-roll: at least one horizon (steady state: every env past its staggered first episode),
+    extended so that the timed window [preroll + warmup, preroll + warmup + steps) holds a horizon
+    boundary -- step k with (k + 1) % horizon == 0, where the episode totals are all-gathered -- near
+    its middle: any --steps >= 1 times one exchange (the collective is part of the timed workload)"""
+    t = max(1, steps // 2)
+    return horizon + (-(warmup + t)) % horizon
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--preroll", type=int, default=-1,
-                    help="untimed steps after the staggered reset (default: one horizon), so the timed "
-                         "window starts in steady state")
+                    help="untimed steps after the staggered reset (default: one horizon plus the offset that "
+                         "puts a horizon boundary -- the episode-totals exchange -- inside the timed window), "
+                         "so the timed window starts in steady state")
     ap.add_argument("--envs-per-gpu", type=int, default=65536)
     ap.add_argument("--total-envs", type=int, default=0,
                     help="strong scaling: fixed total envs split over the ranks (e.g. 262144, SURVEY C4)")
@@ -416,7 +426,9 @@ def main():
         if (k + 1) % sim.horizon == 0:
             gather()
 
-    preroll = sim.horizon if args.preroll < 0 else args.preroll
+    preroll = default_preroll(sim.horizon, args.warmup, args.steps) if args.preroll < 0 else args.preroll
+    exch_steps = [k for k in range(preroll + args.warmup, preroll + args.warmup + args.steps)
+                  if (k + 1) % sim.horizon == 0]
     for k in range(preroll + args.warmup):
         one_step(k)
     e0, r0, s0 = (x.clone() for x in gather())
@@ -444,7 +456,9 @@ def main():
         dist.all_reduce(rank_sums, op=dist.ReduceOp.SUM)
     exchange = dict(backend=dist.get_backend() if pg else "local copy", world=world, collective="all_gather_into_tensor"
                     if pg else None, calls=totals.calls, bytes_per_rank_per_call=totals.bytes_per_rank,
-                    every_steps=sim.horizon, global_episodes=int(e1.long().sum()),
+                    every_steps=sim.horizon, calls_in_timed_window=len(exch_steps),
+                    timed_window_steps=[preroll + args.warmup, preroll + args.warmup + args.steps - 1],
+                    exchange_steps_in_window=exch_steps, global_episodes=int(e1.long().sum()),
                     global_successes=int(s1.long().sum()),
                     gathered_equals_rank_sums=bool(int(e1.long().sum()) == int(rank_sums[0])
                                                    and int(s1.long().sum()) == int(rank_sums[1])))

@@ -92,6 +92,14 @@ int aw_set_option(aw_handle* h, int disableflags, int iterations, int noslip_ite
  * compare the two tiers on the same inputs.  Waits for the device. */
 int aw_set_tier(aw_handle* h, int mode);
 
+/* Fault injection (test hook: the parity classifier's negative tests, tests/test_gpu_classifier.py;
+ * never set by the product).  kind 0: none (the model table as built); kind 1: the margin of every
+ * sphere / capsule pair (collider class 1) shifted by arg x 1e-6 m -- contact activation, the fp64
+ * near-margin decision, the rows' includemargin and the broadphase radius; kind 2: frictionloss row
+ * `arg` (dof order) held in the stick state (its frictionloss limit raised to 1e6, so mj_solNewton's
+ * row never enters a linear zone and noslip never lets it slide).  Waits for the device. */
+int aw_set_fault(aw_handle* h, int kind, int arg);
+
 /* Reset envs (mask[e] != 0, or all if mask == NULL): qpos = qpos0, qvel = 0, warmstart = 0,
  * per-env model params from `params` [N][nparam] or, if NULL, sampled on device (Philox,
  * keyed by seed, global env id and episode count) from the reference reset distribution;

@@ -68,6 +68,9 @@ def load():
     L.aw_random_actions.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp]
     L.aw_set_env_offset.argtypes = [_vp, ctypes.c_uint64]
     L.aw_set_tier.argtypes = [_vp, ctypes.c_int]
+    if hasattr(L, "aw_set_fault"):
+        L.aw_set_fault.argtypes = [_vp, ctypes.c_int, ctypes.c_int]
+        L.aw_set_fault.restype = ctypes.c_int
     L.aw_clear_status.argtypes = [_vp, _vp]
     L.aw_episode_totals.argtypes = [_vp, _vp, _vp, _vp, _vp]
     L.aw_get_episode.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp]
@@ -102,7 +105,7 @@ def load():
     return L
 
 
-EXPORTS = ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_set_tier", "aw_reset", "aw_step",
+EXPORTS = ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_set_tier", "aw_set_fault", "aw_reset", "aw_step",
            "aw_random_actions", "aw_set_env_offset", "aw_get_state", "aw_set_state", "aw_status",
            "aw_clear_status", "aw_episode_stats", "aw_episode_totals", "aw_set_episode_totals", "aw_get_episode",
            "aw_set_episode",
@@ -221,6 +224,11 @@ class Sim:
     def set_tier(self, mode: int):
         """0: automatic (fast tier, wide tier for overflowing env-steps); 1: wide tier only (tests)"""
         _check(load().aw_set_tier(self.h, int(mode)))
+
+    def set_fault(self, kind: int, arg: int = 0):
+        """test hook (include/adroit_wave.h aw_set_fault): 0 none, 1 class-1 margins + arg um,
+        2 frictionloss row `arg` held in the stick state"""
+        _check(load().aw_set_fault(self.h, int(kind), int(arg)))
 
     def reset(self, obs, params=None, mask=None, seed: int = 1):
         _check(load().aw_reset(self.h, _ptr(mask), _ptr(params), seed, _ptr(obs), _stream()))

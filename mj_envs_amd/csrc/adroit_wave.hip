@@ -1065,6 +1065,10 @@ struct aw_handle {
   void* dmhdr_wide = nullptr;   // the wide tier's header: m with jspill -> jspill_wide, then st
   float* jspill_wide = nullptr; // one JSPILL_WIDE block per wide workgroup
   int wide_grid = 0;            // persistent k_step_wide workgroups (resident slots, capped at nenv)
+  // aw_set_fault: the model table's pair margins / broadphase radii as built (restored by kind 0)
+  std::vector<float> fault_margin0, fault_rb0;
+  std::vector<double> fault_margin64_0;
+  std::vector<int> fault_cls;
 };
 
 #ifndef AW_TASK_TU
@@ -1111,6 +1115,7 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
   m.nparam = B.dim("task_nparam", 0); m.variation = B.dim("task_variation", 0);
   if (m.nparam > MAXP) return fail(AW_EUNSUPPORTED, "too many per-env params");
   m.disableflags = 0;
+  m.fault_flrow = -1;
 
   std::vector<int> parent = B.i("body_parentid"), rootid = B.i("body_rootid"), dofnum = B.i("body_dofnum"),
                    dofadr = B.i("body_dofadr");
@@ -1702,6 +1707,41 @@ int aw_set_tier(aw_handle* h, int mode) {
   h->m.force_wide = mode;
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipDeviceSynchronize());   // queued launches read the old header
+  return upload_header(h);
+}
+
+int aw_set_fault(aw_handle* h, int kind, int arg) {
+  if (!h || kind < 0 || kind > 2) return fail(AW_EINVAL, "aw_set_fault: kind must be 0 (none), 1 (margin) or 2 (stick row)");
+  if (kind == 2 && (arg < 0 || arg >= h->m.nfl)) return fail(AW_EINVAL, "aw_set_fault: no such frictionloss row");
+  if (kind == 1 && (arg < -1000 || arg > 1000)) return fail(AW_EINVAL, "aw_set_fault: margin shift beyond 1 mm");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipDeviceSynchronize());   // queued launches read the old table / header
+  MData* dm = (MData*)h->dmodel;
+  const int np = h->m.npairall;
+  if (h->fault_cls.empty()) {      // the table as built, saved once
+    h->fault_margin0.resize(np); h->fault_rb0.resize(np); h->fault_margin64_0.resize(np); h->fault_cls.resize(np);
+    HIPCHK(hipMemcpy(h->fault_margin0.data(), dm->cp_margin, np * sizeof(float), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h->fault_rb0.data(), dm->cp_rb, np * sizeof(float), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h->fault_margin64_0.data(), dm->cp_margin64, np * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h->fault_cls.data(), dm->cp_class, np * sizeof(int), hipMemcpyDeviceToHost));
+  }
+  std::vector<float> mg = h->fault_margin0, rb = h->fault_rb0;
+  std::vector<double> mg64 = h->fault_margin64_0;
+  if (kind == 1) {
+    // every sphere / capsule pair (collider class 1): activation, the fp64 decision, the rows'
+    // includemargin and the broadphase radius all see the shifted margin
+    const double dl = 1e-6 * arg;
+    for (int p = 0; p < np; p++)
+      if (h->fault_cls[p] == 1) {
+        mg64[p] += dl;
+        mg[p] = (float)mg64[p];
+        rb[p] = (float)((double)rb[p] + dl);
+      }
+  }
+  HIPCHK(hipMemcpy(dm->cp_margin, mg.data(), np * sizeof(float), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dm->cp_rb, rb.data(), np * sizeof(float), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dm->cp_margin64, mg64.data(), np * sizeof(double), hipMemcpyHostToDevice));
+  h->m.fault_flrow = kind == 2 ? arg : -1;
   return upload_header(h);
 }
 

@@ -54,16 +54,25 @@ namespace aw {
 // (r05q A/B).  The host allocates the spill blocks for the largest value.
 constexpr int fast_maxdense_of(int task) { return task == 3 ? 192 : 128; }
 constexpr int FAST_MAXDENSE_ALLOC = 192;
+// The value is a preprocessor literal (AW_FAST_MD) because it also names the fast tier's inline
+// namespace (fast128 / fast192 below): relocate's task unit and the others compile Env -- and every
+// always-inline function taking one -- at different sizes, so their mangled names must differ too.
 #if defined(AW_FAST_MAXDENSE)
-#elif defined(AW_TASK_TU)
-#define AW_FAST_MAXDENSE fast_maxdense_of(AW_TASK_TU)
-#elif defined(AW_ONLY_TASK)
-#define AW_FAST_MAXDENSE fast_maxdense_of(AW_ONLY_TASK)
+#define AW_FAST_MD AW_FAST_MAXDENSE   // explicit override (tools/build_variant.py): a literal
+#elif (defined(AW_TASK_TU) && AW_TASK_TU == 3) || (defined(AW_ONLY_TASK) && AW_ONLY_TASK == 3)
+#define AW_FAST_MD 192
 #else
-#define AW_FAST_MAXDENSE 128   // single-TU builds of all four tasks (diagnostics): one Env for all
+#define AW_FAST_MD 128   // the other tasks, the API unit, single-TU builds of all four tasks
 #endif
-constexpr int FAST_MAXCON = 48, FAST_NRL = 3, FAST_MAXDENSE = AW_FAST_MAXDENSE;
+#if defined(AW_TASK_TU) && !defined(AW_FAST_MAXDENSE)
+static_assert(AW_FAST_MD == fast_maxdense_of(AW_TASK_TU), "fast_maxdense_of and AW_FAST_MD disagree");
+#elif defined(AW_ONLY_TASK) && !defined(AW_FAST_MAXDENSE)
+static_assert(AW_FAST_MD == fast_maxdense_of(AW_ONLY_TASK), "fast_maxdense_of and AW_FAST_MD disagree");
+#endif
+constexpr int FAST_MAXCON = 48, FAST_NRL = 3, FAST_MAXDENSE = AW_FAST_MD;
 static_assert(FAST_MAXDENSE <= FAST_MAXDENSE_ALLOC, "fast spill blocks are allocated for FAST_MAXDENSE_ALLOC");
+#define AW_CAT2(a, b) a##b
+#define AW_CAT(a, b) AW_CAT2(a, b)
 constexpr int WIDE_MAXCON = 100, WIDE_NRL = 8, WIDE_MAXDENSE = 500;
 constexpr int NCONMAX = 100, NJMAX = 500;   // the reference model's caps (DAPG_assets.xml:4)
 #ifdef AW_WIDE
@@ -74,7 +83,7 @@ constexpr int NRL = WIDE_NRL;         // constraint rows per lane in the Newton 
 constexpr int EFC_CAP = NJMAX;        // rows kept (MuJoCo's njmax), storage MAXEFC >= EFC_CAP
 constexpr int MAXDENSE = WIDE_MAXDENSE;
 #else
-inline namespace fast {
+inline namespace AW_CAT(fast, AW_FAST_MD) {   // fast128 / fast192
 constexpr bool WIDE = false;
 constexpr int MAXCON = FAST_MAXCON;   // contacts per env (one lane each in the sort)
 constexpr int NRL = FAST_NRL;         // constraint rows per lane in the Newton solver
@@ -96,7 +105,7 @@ constexpr int JSPILL_FAST = (FAST_MAXDENSE_ALLOC - 32) * VS, JSPILL_WIDE = (WIDE
 #ifdef AW_WIDE
 #define AW_TIER wide
 #else
-#define AW_TIER fast
+#define AW_TIER AW_CAT(fast, AW_FAST_MD)
 #endif
 
 constexpr float MINVAL = 1e-15f;
@@ -270,6 +279,7 @@ struct DModel {
   int cls_start[NCLASS + 1];  // collider class c owns pair-list slots [cls_start[c], cls_start[c+1])
   int nrgeom;                 // rendered geoms
   int force_wide;             // test hook (aw_set_tier): every forward of the fast tier defers to the wide tier
+  int fault_flrow;            // test hook (aw_set_fault, kind 2): this frictionloss row never slides; -1: off
   const MData* __restrict__ d;
   float* jspill;              // dense-J rows past JL, one block of the tier's JSPILL floats per workgroup slot (device)
   unsigned long long env_offset;   // global id of env 0 of this handle (shards): Philox keys

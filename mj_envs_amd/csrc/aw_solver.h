@@ -263,7 +263,9 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
     int d = MD(fl_dof, lane);
     s.efc_type[lane] = C_FRIC_DOF; s.efc_id[lane] = d;
     s.efc_i0[lane] = d; s.efc_i1[lane] = -1; s.efc_v0[lane] = 1.f; s.efc_v1[lane] = 0.f;
-    s.rowbuf[lane] = 0.f; s.efc_floss[lane] = MD(dof_frictionloss, d); s.efc_force[lane] = MD(dof_invweight0, d);
+    // (aw_set_fault kind 2, the parity classifier's negative test: one row held in the stick state)
+    s.rowbuf[lane] = 0.f; s.efc_floss[lane] = lane == m.fault_flrow ? 1e6f : MD(dof_frictionloss, d);
+    s.efc_force[lane] = MD(dof_invweight0, d);
   }
   // joint limits: lower then upper per joint, joints in order.  MuJoCo activates a side when
   // dist = side * (range - q) < margin, in fp64.  That test is evaluated here in fp64 too, on the

@@ -66,6 +66,12 @@ void or_set_option(void* p, int disableflags, int max_con, int max_efc, int iter
   init_data(&h->m, &h->d1);
 }
 
+/* test hook: shift the margin of one geom pair (model geom ids, either order; g1 < 0 clears) */
+void or_set_margin_nudge(void* p, int g1, int g2, double delta) {
+  Handle* h = (Handle*)p;
+  h->m.nudge_g1 = g1; h->m.nudge_g2 = g2; h->m.nudge_delta = g1 < 0 ? 0.0 : delta;
+}
+
 int or_dims(void* p, int* out) {
   const Model& m = ((Handle*)p)->m;
   int v[] = {m.nq, m.nv, m.nu, m.nbody, m.ngeom, m.nsite, m.task_obs_dim, m.task_nparam,

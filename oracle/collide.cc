@@ -852,6 +852,10 @@ static void finish_contacts(Data* d, int start, int g1, int g2, int condim, cons
   }
 }
 
+static num nudge(const Model* m, int g1, int g2) {
+  return (g1 == m->nudge_g1 && g2 == m->nudge_g2) || (g1 == m->nudge_g2 && g2 == m->nudge_g1) ? m->nudge_delta : 0;
+}
+
 void collision(const Model* m, Data* d) {
   d->ncon = 0;
   if (m->disableflags & (DSBL_CONSTRAINT | DSBL_CONTACT)) return;
@@ -859,7 +863,7 @@ void collision(const Model* m, Data* d) {
   /* explicit pairs */
   for (int p = 0; p < m->npair; p++) {
     int g1 = m->pair_geom1[p], g2 = m->pair_geom2[p];
-    num margin = m->pair_margin[p];
+    num margin = m->pair_margin[p] + nudge(m, g1, g2);
     int n = collide_geoms(m, d, g1, g2, margin, buf, 16);
     int start = d->ncon;
     for (int k = 0; k < n; k++) {
@@ -872,7 +876,7 @@ void collision(const Model* m, Data* d) {
   /* dynamic candidates */
   for (int c = 0; c < m->ncand; c++) {
     int g1 = m->cand_geom1[c], g2 = m->cand_geom2[c];
-    num margin = std::fmax(m->geom_margin[g1], m->geom_margin[g2]);
+    num margin = std::fmax(m->geom_margin[g1], m->geom_margin[g2]) + nudge(m, g1, g2);
     num gap = std::fmax(m->geom_gap[g1], m->geom_gap[g2]);
     int n = collide_geoms(m, d, g1, g2, margin, buf, 16);
     if (!n) continue;

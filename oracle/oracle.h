@@ -66,6 +66,10 @@ struct Model {
   int iterations, noslip_iterations, mpr_iterations;
   int disableflags;
   int max_con, max_efc;
+  /* test hook (or_set_margin_nudge): the margin of the geom pair (nudge_g1, nudge_g2), either order,
+   * shifted by nudge_delta -- the parity classifier's causal check of a near-margin contact */
+  int nudge_g1 = -1, nudge_g2 = -1;
+  num nudge_delta = 0;
 
   std::vector<int> body_parentid, body_rootid, body_weldid, body_jntnum, body_jntadr, body_dofnum,
       body_dofadr, body_mocap;

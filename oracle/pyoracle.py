@@ -39,6 +39,7 @@ def lib():
         L.or_destroy.argtypes = [ctypes.c_void_p]
         L.or_set_option.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 5
         L.or_dims.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        L.or_set_margin_nudge.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_double]
         L.or_reset.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, ctypes.c_int]
         L.or_step.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _u8p,
                               _u8p, _u32p, ctypes.c_int]
@@ -87,6 +88,10 @@ class Oracle:
     def set_option(self, disableflags=-1, max_con=-1, max_efc=-1, iterations=-1, noslip_iterations=-1):
         lib().or_set_option(self.h, disableflags, max_con, max_efc, iterations, noslip_iterations)
         self._dims()
+
+    def set_margin_nudge(self, g1: int = -1, g2: int = -1, delta: float = 0.0):
+        """shift the margin of the geom pair (g1, g2) (model geom ids) by delta; g1 < 0 clears"""
+        lib().or_set_margin_nudge(self.h, int(g1), int(g2), float(delta))
 
     def __del__(self):
         try:

@@ -197,3 +197,16 @@ def test_bench_launcher_one_gpu_rccl():
     assert x["gathered_equals_rank_sums"]
     assert x["global_episodes"] >= 4096                   # every env ended >= 1 episode in the pre-roll
     assert 0 < d["episodes"]["finished_in_timed_window"] <= 4096
+
+
+def test_bench_default_preroll_times_one_exchange():
+    """whatever --warmup / --steps the driver passes, the default pre-roll puts one
+    horizon boundary (the episode-totals all-gather) inside the timed window"""
+    from bench import default_preroll
+    for horizon in (100, 200):
+        for warmup in (0, 5, 20, 300):
+            for steps in (1, 2, 20, 400, 1000):
+                p = default_preroll(horizon, warmup, steps)
+                window = range(p + warmup, p + warmup + steps)
+                assert p >= horizon
+                assert any((k + 1) % horizon == 0 for k in window), (horizon, warmup, steps, p)

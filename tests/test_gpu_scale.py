@@ -123,13 +123,23 @@ def test_wide_tier_reset_and_set_state_forward():
 C3_FULL_MIN = 0.995
 
 
+# relocate runs with bench.py's own seeds and phases (reset seed 1, Philox action seed 0, the bench's
+# stagger_phases) for 420 env-steps -- the bench's pre-roll, warm-up and timed window --, the regime in
+# which its config-3 line sends envs past the fast capacities (r05zz: 2 per run): the wide tier's
+# env-steps are then teacher-forced in the reference's own regime, and their count is asserted, so
+# the branch cannot go silently dead.  door / pen never leave their fast tier under random actions.
+C3_RUN = {"door-v0": (7, 9, 200, False), "pen-v0": (7, 9, 200, False), "relocate-v0": (1, 0, 420, True)}
+
+
 @pytest.mark.parametrize("env_id", ["door-v0", "pen-v0", "relocate-v0"])
 def test_config3_full_size_16384_envs(env_id):
-    """BASELINE configs[2] at its real size: 16 384 envs, grid < n (persistent claims), 200
-    env-steps with auto-reset from staggered phases.  Zero envs drop a constraint MuJoCo keeps;
-    teacher forcing on 256 sampled envs + every env-step the wide tier ran."""
+    """BASELINE configs[2] at its real size: 16 384 envs, grid < n (persistent claims), 200 (relocate:
+    420) env-steps with auto-reset from staggered phases.  Zero envs drop a constraint MuJoCo keeps;
+    teacher forcing on 256 sampled envs + every env-step the wide tier ran (relocate: at least one)."""
     from mj_envs_amd import _native
-    n, steps = 16384, 200
+    from mj_envs_amd.dist import stagger_phases
+    n = 16384
+    seed_reset, seed_act, steps, bench_phases = C3_RUN[env_id]
     m, o = make_oracle(env_id)
     _, sim = _sim(env_id, n)
     assert sim.grid < n, f"grid {sim.grid} covers all {n} envs: the persistent claim path is not exercised"
@@ -137,8 +147,9 @@ def test_config3_full_size_16384_envs(env_id):
     # the fast tier's dense rows: relocate's own TU holds 192 (aw_common.h fast_maxdense_of)
     assert sim.fast_maxdense == (192 if env_id == "relocate-v0" else 128), sim.fast_maxdense
     obs, rew, done, goal = _bufs(sim, n)
-    sim.reset(obs, seed=7)
-    sim.set_episode(ep_len=torch.from_numpy((np.arange(n) * 7919 % sim.horizon).astype(np.int32)).cuda())
+    sim.reset(obs, seed=seed_reset)
+    phases = stagger_phases(n, 0, sim.horizon) if bench_phases else (np.arange(n) * 7919 % sim.horizon).astype(np.int32)
+    sim.set_episode(ep_len=torch.from_numpy(phases).cuda())
     sim.clear_status()
     idx = np.unique(np.linspace(0, n - 1, 256).round().astype(int))
     q, v, w, p = sim.empty(n, sim.nq), sim.empty(n, sim.nv), sim.empty(n, sim.nv), sim.empty(n, sim.nparam)
@@ -151,8 +162,8 @@ def test_config3_full_size_16384_envs(env_id):
         torch.cuda.synchronize()
         pre = dict(qpos=q.cpu().numpy().astype(np.float64), qvel=v.cpu().numpy().astype(np.float64),
                    warm=w.cpu().numpy().astype(np.float64), params=p.cpu().numpy().astype(np.float64))
-        sim.random_actions(act, 9, k)
-        sim.step(act, obs, rew, done, goal, autoreset=True, seed=7)
+        sim.random_actions(act, seed_act, k)
+        sim.step(act, obs, rew, done, goal, autoreset=True, seed=seed_reset)
         sim.get_state(q, v)
         sim.status(last)
         torch.cuda.synchronize()
@@ -189,9 +200,11 @@ def test_config3_full_size_16384_envs(env_id):
           f"envs dropping constraints at MuJoCo's caps: {n_over}")
     err = _err_report(label, np.concatenate(eqs), np.concatenate(evs), ok)
     _hard_cap(np.concatenate(eqs), np.concatenate(evs), label)
-    unexplained = _classify_misses(env_id, misses, sim.frame_skip)
+    unexplained = _classify_misses(env_id, misses, label=label)
     print(f"{label}: {len(misses)} misses, unexplained: {unexplained}")
     assert n_over == 0, f"{n_over} envs dropped constraints"
+    if env_id == "relocate-v0":
+        assert wide_cases >= 1, "no wide-tier env-step was compared: the over-capacity branch went untested"
     assert frac >= C3_FULL_MIN and rfrac >= REWARD_MIN, (frac, rfrac)
     assert not unexplained, unexplained
     _err_gate(err)
@@ -202,9 +215,13 @@ def test_config3_full_size_16384_envs(env_id):
 # within 1e-6 of its margin, 126 a contact / row set that differs); deciding near-margin sphere /
 # capsule contacts on fp64 frames (stage_collision) brought it to 0.9980 (r05f: 41 misses, 22 at a
 # margin, 8 a contact / row set, 11 an fp32-unstable reference), i.e. at the target to one case.
-# The gate is a floor under the measurement; the target is printed beside it.
+# VERDICT r04's target for this regime is 0.998; the measurement is 41 misses of 20 480 = 0.997998, one
+# case short of it (r05zg, r06e), every miss classified with causal evidence (tests/parity_classify.py:
+# 25 contacts at their margin whose 2e-6 m margin shift moves the reference by more than the GPU's
+# deviation, 13 oracle-shadowed trajectories, ...).  The assertion is the floor under the measurement;
+# the target is printed beside it and DESIGN.md reports it as not met.
 DAPG_HEADLINE_MIN = 0.998
-DAPG_HEADLINE_FLOOR = 0.995
+DAPG_HEADLINE_FLOOR = 0.9975
 
 
 def _dapg_teacher_forced(env_id, n, warm_steps, steps, seed):
@@ -256,7 +273,7 @@ def _dapg_teacher_forced(env_id, n, warm_steps, steps, seed):
     print(f"{label}: {frac:.4f} of {ok.size} sampled (env, step) cases within tolerance, rewards {rfrac:.4f}")
     err = _err_report(label, np.concatenate(eqs), np.concatenate(evs), ok)
     _hard_cap(np.concatenate(eqs), np.concatenate(evs), label)
-    unexplained = _classify_misses(env_id, misses, sim.frame_skip)
+    unexplained = _classify_misses(env_id, misses, label=label)
     print(f"{label}: {len(misses)} misses at steps {sorted(set(ms[0] for ms in misses))}, unexplained: {unexplained}")
     _, sticky = _status(sim, n)
     return label, frac, rfrac, err, unexplained, sticky
@@ -268,10 +285,10 @@ def test_dapg_teacher_forced_headline_size():
     from mj_envs_amd import _native
     label, frac, rfrac, err, unexplained, sticky = _dapg_teacher_forced("hammer-v0", 65536, 40, 80, 31)
     assert not ((sticky & _native.ST_OVERFLOW) != 0).any()
+    print(f"{label}: DAPG_HEADLINE_MIN target {DAPG_HEADLINE_MIN}: {'met' if frac >= DAPG_HEADLINE_MIN else 'NOT met'}")
     assert frac >= DAPG_HEADLINE_FLOOR and rfrac >= REWARD_MIN, (frac, rfrac)
     assert not unexplained, unexplained
     _err_gate(err)
-    print(f"{label}: DAPG_HEADLINE_MIN target {DAPG_HEADLINE_MIN}: {'met' if frac >= DAPG_HEADLINE_MIN else 'NOT met'}")
 
 
 # door / pen / relocate in their DAPG grasp regimes at BASELINE config 3's size (16 384 envs,

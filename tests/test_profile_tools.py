@@ -72,7 +72,7 @@ def test_kernel_name_match_excludes_wide_tier():
     """k_step's counters must not absorb the wide tier's drain kernel (k_step_wide launches after
     every k_step, usually on an empty queue) or the profiling TU's variants"""
     import summarize_profiles as sp
-    assert sp.is_kernel("void aw::fast::k_step<0>(aw::DModel, float*)", "k_step")
+    assert sp.is_kernel("void aw::fast128::k_step<0>(aw::DModel, float*)", "k_step")
     assert sp.is_kernel("k_step<2>", "k_step")
     assert not sp.is_kernel("void aw::wide::k_step_wide<0>(aw::DModel, float*)", "k_step")
     assert sp.is_kernel("k_step_wide<0>", "k_step_wide")

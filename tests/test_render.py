@@ -112,3 +112,47 @@ def test_gpu_depth_vs_checker(env_id):
         ok = np.abs(D[e] - R) <= 2e-3
         assert ok.mean() >= 0.995, (env_id, e, ok.mean(), np.abs(D[e] - R).max())
         assert (D[e] < cam[16]).mean() > 0.5      # the scene fills the frame
+
+
+@pytest.mark.gpu
+def test_gpu_depth_config5_size():
+    """BASELINE config 5 at its own size (hammer-v0 + 64x64 depth, 8 192 envs): a 60-step random
+    rollout with auto-reset from staggered episode phases (the bench's regime), then the depth frames
+    of 64 envs sampled evenly across the whole batch against the fp64 checker."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mj_envs_amd import _native
+    from mj_envs_amd.render import free_camera
+    from oracle.depth import oracle_geoms, render_depth
+    env_id, n, W, H, steps = "hammer-v0", 8192, 64, 64, 60
+    m, orc = make_oracle(env_id)
+    sim = _native.Sim(m.to_blob(), n)
+    obs = sim.empty(n, sim.obs_dim)
+    sim.reset(obs, seed=11)
+    sim.set_episode(ep_len=torch.from_numpy((np.arange(n) * 7919 % sim.horizon).astype(np.int32)).cuda())
+    act = sim.empty(n, sim.nu)
+    rew, done, goal = sim.empty(n), sim.empty(n, dtype=torch.uint8), sim.empty(n, dtype=torch.uint8)
+    cam = free_camera(m, env_id, W, H)
+    depth = sim.empty(n, H, W)
+    for k in range(steps):
+        sim.random_actions(act, 13, k)
+        sim.step(act, obs, rew, done, goal, autoreset=True, seed=11)
+        sim.render_depth(depth, cam)          # every env-step, as bench.py --depth times it
+    qpos, qvel = sim.empty(n, sim.nq), sim.empty(n, sim.nv)
+    params = sim.empty(n, sim.nparam)
+    sim.get_state(qpos, qvel, None, params)
+    torch.cuda.synchronize()
+    idx = np.unique(np.linspace(0, n - 1, 64).round().astype(int))
+    D = depth.cpu().numpy()[idx]
+    assert np.isfinite(D).all()
+    Q, V, Pm = (x.cpu().numpy().astype(np.float64)[idx] for x in (qpos, qvel, params))
+    fr = []
+    for j in range(len(idx)):
+        orc.forward1(Pm[j], Q[j], V[j])
+        R = render_depth(cam, W, H, oracle_geoms(orc, m))
+        ok = np.abs(D[j] - R) <= 2e-3
+        fr.append(ok.mean())
+        assert ok.mean() >= 0.995, (int(idx[j]), ok.mean(), np.abs(D[j] - R).max())
+        assert (D[j] < cam[16]).mean() > 0.5
+    print(f"config 5 depth: {len(idx)} envs of {n}, pixels within 2e-3 m: min {min(fr):.4f}, mean {np.mean(fr):.4f}")
