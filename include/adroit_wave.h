@@ -176,6 +176,11 @@ int aw_task_eval(aw_handle* h, int n, const float* qpos, const float* qvel, cons
  * AW_DUMP_SIZE floats; layout: mj_envs_amd/_native.py DUMP_LAYOUT). */
 #define AW_DUMP_SIZE 3400
 int aw_forward_dump(aw_handle* h, int env, const float* ctrl, float* out, void* stream);
+/* The same forward through the wide-capacity tier (MuJoCo's nconmax 100 / njmax 500: contacts and
+ * rows past the fast tier's capacities are kept), AW_DUMP_SIZE_WIDE floats, the layout of
+ * dump_layout(128, 512). */
+#define AW_DUMP_SIZE_WIDE 6120
+int aw_forward_dump_wide(aw_handle* h, int env, const float* ctrl, float* out, void* stream);
 
 /* Depth camera observation (the reference renders RGB through OpenGL:
  * headless_observer.py:20-52 -- free camera azimuth 90, distance 4.5, elevation from the

@@ -38,6 +38,9 @@ def dump_layout(maxcon=MAXCON, maxefc=MAXEFC):
 
 
 DUMP_LAYOUT = dump_layout()
+WIDE_MAXCON_STORE, WIDE_MAXEFC = 128, 512       # the wide tier's contact storage and row slots
+DUMP_LAYOUT_WIDE = dump_layout(WIDE_MAXCON_STORE, WIDE_MAXEFC)
+AW_DUMP_SIZE_WIDE = 1768 + 14 * WIDE_MAXCON_STORE + 5 * WIDE_MAXEFC
 # why the Newton solve stopped (aw_solver.h NT_EXIT_*)
 NT_EXIT = ("max_iterations", "no_descent", "fp32_noise_floor", "improvement", "gradient", "no_constraints")
 AW_DUMP_SIZE = 1768 + 14 * MAXCON + 5 * MAXEFC
@@ -68,6 +71,9 @@ def load():
     L.aw_random_actions.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp]
     L.aw_set_env_offset.argtypes = [_vp, ctypes.c_uint64]
     L.aw_set_tier.argtypes = [_vp, ctypes.c_int]
+    if hasattr(L, "aw_forward_dump_wide"):
+        L.aw_forward_dump_wide.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp]
+        L.aw_forward_dump_wide.restype = ctypes.c_int
     if hasattr(L, "aw_set_fault"):
         L.aw_set_fault.argtypes = [_vp, ctypes.c_int, ctypes.c_int]
         L.aw_set_fault.restype = ctypes.c_int
@@ -109,7 +115,7 @@ EXPORTS = ("aw_create", "aw_destroy", "aw_dims", "aw_set_option", "aw_set_tier",
            "aw_random_actions", "aw_set_env_offset", "aw_get_state", "aw_set_state", "aw_status",
            "aw_clear_status", "aw_episode_stats", "aw_episode_totals", "aw_set_episode_totals", "aw_get_episode",
            "aw_set_episode",
-           "aw_task_eval", "aw_forward_dump", "aw_stage_profile", "aw_render_depth", "aw_policy_mlp",
+           "aw_task_eval", "aw_forward_dump", "aw_forward_dump_wide", "aw_stage_profile", "aw_render_depth", "aw_policy_mlp",
            "aw_collide_test", "aw_last_error")
 
 STAGES = ("pre", "kinematics", "collision", "com_crb", "rne_smooth_solve", "constraints", "newton",
@@ -305,12 +311,14 @@ class Sim:
         c = cnt.cpu().numpy()
         return [o[i, :c[i]] for i in range(n)]
 
-    def forward_dump(self, env: int, ctrl=None) -> dict:
-        import torch
-        out = self.empty(AW_DUMP_SIZE)
-        _check(load().aw_forward_dump(self.h, env, _ptr(ctrl), _ptr(out), _stream()))
+    def forward_dump(self, env: int, ctrl=None, wide: bool = False) -> dict:
+        """one forward of env `env` (ctrl: raw controls or None = 0) and its internals; wide=True runs it
+        through the wide-capacity tier (aw_forward_dump_wide: MuJoCo's nconmax / njmax)"""
+        out = self.empty(AW_DUMP_SIZE_WIDE if wide else AW_DUMP_SIZE)
+        fn = load().aw_forward_dump_wide if wide else load().aw_forward_dump
+        _check(fn(self.h, env, _ptr(ctrl), _ptr(out), _stream()))
         o = out.cpu().numpy().astype(np.float64)
-        res = {k: o[a:a + n] for k, (a, n) in DUMP_LAYOUT.items()}
+        res = {k: o[a:a + n] for k, (a, n) in (DUMP_LAYOUT_WIDE if wide else DUMP_LAYOUT).items()}
         nv, nb, ns = self.nv, self.nbody, self.nsite
         res["xpos"] = res["xpos"][:3 * nb].reshape(nb, 3)
         res["xquat"] = res["xquat"][:4 * nb].reshape(nb, 4)

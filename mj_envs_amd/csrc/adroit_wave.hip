@@ -114,7 +114,11 @@ AW_DEV void sort_contacts(Env& s, int lane) {
       copy3(s.con_nrm[r], nrm[h]);
     }
   }
-  if (lane == 0) s.ncon = n - (int)s.kin64_mask;   // fp64-dropped candidates sorted last (stage_collision)
+  if (lane == 0) {
+    s.ncon = n - (int)s.kin64_mask;   // fp64-dropped candidates sorted last (stage_collision)
+    // the wide tier's nconmax applies to the decided contacts, in pair order (mj_collision)
+    if (s.ncon > CON_CAP) { s.ncon = CON_CAP; s.status |= ST_CON_OVERFLOW; }
+  }
   wsync();
 }
 
@@ -505,6 +509,13 @@ struct StepIO {
   const int* perm;   // claim position -> env (k_order: each XCD class's envs, most expensive first)
   unsigned long long t0;   // this workgroup's current env-step start (s_memtime)
 };
+// LDS budgets (one wave per workgroup): the fast tier's Env + StepIO inside the 20 480-byte granule
+// that gives eight envs per CU (two waves per SIMD); the wide tier's inside 40 KiB (four per CU, one
+// wave per SIMD).  A layout change that breaks either is a compile error, not an occupancy surprise.
+static_assert(WIDE || sizeof(Env) + sizeof(StepIO) <= 20480, "fast-tier LDS past the two-waves-per-SIMD budget");
+static_assert(!WIDE || sizeof(Env) + sizeof(StepIO) <= 40960, "wide-tier LDS past the one-wave-per-SIMD budget");
+static_assert(sizeof(((Env*)nullptr)->rowbuf) / sizeof(float) >= 64 * FAST_NRL, "row buffer holds the observation");
+
 AW_DEV void park_io(StepIO& io, int lane, const float* actions, float* obs, float* reward, uint8_t* done,
                     uint8_t* goal, float* terminal_obs, int autoreset, uint64_t seed, int* defer) {
   if (lane == 0) {
@@ -778,32 +789,123 @@ __global__ void __launch_bounds__(64) k_set_state(DModel m, DState st, int n, co
   if (lane == 0) { st.status[env] = s.status; st.status_acc[env] |= s.status; }
 }
 #else  // AW_WIDE
+#ifdef AW_WIDE_TWO_SITES
+// DIAGNOSTIC ONLY (tools/debug_wide.py, DESIGN.md "the wide-tier hang"): round 5's variant with a
+// second inlined forward call site for the queue's forward-only entries (-DAW_WIDE_TWO_SITES_NOINLINE:
+// the same code as a called function instead)
+#ifdef AW_WIDE_TWO_SITES_NOINLINE
+#define AW_FS_ATTR __device__ __attribute__((noinline))
+#else
+#define AW_FS_ATTR AW_DEV
+#endif
+template <int TASK>
+AW_FS_ATTR void forward_stored(const DModel& m, Env& s, const DState& st, int env, int lane, float* obs) {
+  constexpr int NV = Tree<TASK>::NV;
+  wsync();
+#ifdef AW_TRACE
+  if (lane == 0) printf("forward_stored: env %d st.status %p st.status_acc %p &st %p\n", env, (void*)st.status,
+                        (void*)st.status_acc, (const void*)&st);
+#endif
+  load_env<NV>(m, s, st, env, lane);
+  if (lane == 0) s.status = ST_WIDE;
+  if (lane < m.nu) s.ctrl[lane] = 0.f;
+  stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
+  float Mrow[NV];
+  Dof d;
+  forward<TASK>(m, s, lane, Mrow, d);
+#ifdef AW_TRACE
+  if (lane == 0) printf("forward_stored: env %d forward done, obs %p obs_dim %d\n", env, obs, m.obs_dim);
+#endif
+  if (obs) {
+    task_obs(m, s, lane, s.rowbuf);
+#ifdef AW_TRACE
+    if (lane == 0) printf("forward_stored: task_obs done\n");
+#endif
+    wsync();
+    for (int o = lane; o < m.obs_dim; o += 64) obs[(size_t)env * m.obs_dim + o] = s.rowbuf[o];
+    wsync();
+#ifdef AW_TRACE
+    if (lane == 0) printf("forward_stored: obs stored; env %d st.status %p st.status_acc %p &st %p s.status %u\n", env,
+                          (void*)st.status, (void*)st.status_acc, (const void*)&st, s.status);
+#endif
+  }
+#ifdef AW_TRACE
+  {
+    const unsigned long long ex0 = __builtin_amdgcn_read_exec();
+    if (lane == 0) printf("forward_stored: exec before the status block %llx\n", ex0);
+  }
+#endif
+#ifdef AW_TRACE
+  if (lane == 0) {
+    const unsigned a = st.status[env];
+    printf("forward_stored: status loaded %u\n", a);
+    st.status[env] = a | s.status;
+    printf("forward_stored: status written\n");
+    st.status_acc[env] |= s.status;
+    printf("forward_stored: status_acc written\n");
+  }
+#else
+  if (lane == 0) { st.status[env] |= s.status; st.status_acc[env] |= s.status; }
+#endif
+#ifdef AW_TRACE
+  {
+    // exec as the scalar unit sees it after the block: a zero exec runs no vector instruction (no
+    // printf) and makes the claim loop spin -- restore it only to report
+    const unsigned long long ex = __builtin_amdgcn_read_exec();
+    if (ex != ~0ull) {
+      asm volatile("s_mov_b64 exec, -1" ::: "memory");
+      if (lane == 0) printf("forward_stored: EXEC AFTER THE STATUS BLOCK %llx\n", ex);
+    }
+    if (lane == 0) printf("forward_stored: status stored\n");
+  }
+#endif
+}
+#endif
 // The wide tier: persistent workgroups drain the queue the fast launch before it filled (q[0]
 // entries; an empty queue ends every workgroup at its first claim).  Same env-step code with
 // MuJoCo's capacities; mptr is the wide header (its jspill: one JSPILL_WIDE block per workgroup).
+// The claim loop is bounded by the handle's env count (the queue holds at most one entry per env and
+// launch), so every wave reaches its exit whatever the queue words hold; an entry that is not a valid
+// (env < n, kind DK_STEP / DK_FORWARD) pair is skipped -- -DAW_DEVICE_ASSERT traps instead.
 template <int TASK>
 __global__ void __launch_bounds__(64) k_step_wide(const DModel* __restrict__ mptr, const float* __restrict__ actions,
                                                   float* obs, float* reward, uint8_t* done, uint8_t* goal,
                                                   float* terminal_obs, int autoreset, uint64_t seed,
-                                                  int* __restrict__ q) {
+                                                  int* __restrict__ q, int n) {
   const DModel& m = *mptr;
   const DState& st = *reinterpret_cast<const DState*>(mptr + 1);
   __shared__ Env s;
   __shared__ StepIO io;
   const int lane = threadIdx.x;
   park_io(io, lane, actions, obs, reward, done, goal, terminal_obs, autoreset, seed, nullptr);
-  while (true) {
+  for (int claims = 0; claims <= n; claims++) {
     int k = 0;
     if (lane == 0) k = atomicAdd(q + 1, 1);
     k = __builtin_amdgcn_readfirstlane(k);
 #ifdef AW_TRACE
     if (lane == 0) printf("wide wg %d: claimed %d, q0 %d\n", (int)blockIdx.x, k, q[0]);
 #endif
-    if (k >= q[0]) break;
+    const int nq = q[0];
+#ifdef AW_DEVICE_ASSERT
+    if ((unsigned)nq > (unsigned)n) __builtin_trap();
+#endif
+    if (k >= nq || k >= n) break;
     const int ent = q[2 + k];
     const int env = ent & 0x3fffffff, kind = ent >> 30;
+    if ((unsigned)env >= (unsigned)n || kind > DK_FORWARD) {
+#ifdef AW_DEVICE_ASSERT
+      __builtin_trap();
+#endif
+      continue;
+    }
 #ifdef AW_TRACE
     if (lane == 0) printf("wide wg %d claim %d of %d: env %d kind %d\n", (int)blockIdx.x, k, q[0], env, kind);
+#endif
+#ifdef AW_WIDE_TWO_SITES
+    if (kind == DK_FORWARD) {
+      forward_stored<TASK>(m, s, st, env, lane, io.obs);
+      continue;
+    }
 #endif
     env_step<TASK>(m, s, st, env, lane, io, kind);
   }
@@ -813,12 +915,18 @@ __global__ void __launch_bounds__(64) k_step_wide(const DModel* __restrict__ mpt
 }
 #endif  // AW_WIDE
 
-#ifndef AW_WIDE   // introspection: fast tier only
-// dump layout (floats): see mj_envs_amd/_native.py dump_layout (same offsets from the capacities)
+// introspection: one forward of one env, both tiers (aw_forward_dump / aw_forward_dump_wide)
+// dump layout (floats): see mj_envs_amd/_native.py dump_layout (same offsets from the tier's capacities)
 constexpr int DUMP_SCAL = 1760, DUMP_CON = 1768, DUMP_EFC = DUMP_CON + 14 * MAXCON;
-static_assert(DUMP_EFC + 5 * MAXEFC == AW_DUMP_SIZE, "AW_DUMP_SIZE out of date");
+static_assert(DUMP_EFC + 5 * MAXEFC == (WIDE ? AW_DUMP_SIZE_WIDE : AW_DUMP_SIZE), "AW_DUMP_SIZE(_WIDE) out of date");
+// distinct kernel names per tier: the fast and wide translation units both instantiate it
+#ifdef AW_WIDE
+#define AW_K_DUMP k_dump_wide
+#else
+#define AW_K_DUMP k_dump
+#endif
 template <int TASK>
-__global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const float* ctrl, float* out) {
+__global__ void __launch_bounds__(64) AW_K_DUMP(DModel m, DState st, int env, const float* ctrl, float* out) {
   constexpr int NV = Tree<TASK>::NV;
   __shared__ Env s;
   const int lane = threadIdx.x;
@@ -846,15 +954,15 @@ __global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const
     out[DUMP_SCAL + 3] = (float)s.ndense; out[DUMP_SCAL + 4] = s.touch[0]; out[DUMP_SCAL + 5] = (float)s.status;
     out[DUMP_SCAL + 6] = (float)s.it_newton; out[DUMP_SCAL + 7] = (float)s.it_noslip;
   }
-  if (lane < MAXCON) {
-    bool v = lane < s.ncon;
-    out[DUMP_CON + lane] = v ? s.con_dist[lane] : 0.f;
-    for (int k = 0; k < 3; k++) out[DUMP_CON + MAXCON + 3 * lane + k] = v ? s.con_pos[lane][k] : 0.f;
+  for (int c = lane; c < MAXCON; c += 64) {
+    bool v = c < s.ncon;
+    out[DUMP_CON + c] = v ? s.con_dist[c] : 0.f;
+    for (int k = 0; k < 3; k++) out[DUMP_CON + MAXCON + 3 * c + k] = v ? s.con_pos[c][k] : 0.f;
     float fr[9];
-    for (int k = 0; k < 3; k++) { fr[k] = v ? s.con_nrm[lane][k] : 1.f; fr[3 + k] = 0.f; }
+    for (int k = 0; k < 3; k++) { fr[k] = v ? s.con_nrm[c][k] : 1.f; fr[3 + k] = 0.f; }
     make_frame(fr);
-    for (int k = 0; k < 9; k++) out[DUMP_CON + 4 * MAXCON + 9 * lane + k] = v ? fr[k] : 0.f;
-    out[DUMP_CON + 13 * MAXCON + lane] = v ? (float)s.con_pair[lane] : -1.f;
+    for (int k = 0; k < 9; k++) out[DUMP_CON + 4 * MAXCON + 9 * c + k] = v ? fr[k] : 0.f;
+    out[DUMP_CON + 13 * MAXCON + c] = v ? (float)s.con_pair[c] : -1.f;
   }
   for (int r = lane; r < MAXEFC; r += 64) {
     bool v = r < s.nefc;
@@ -864,8 +972,6 @@ __global__ void __launch_bounds__(64) k_dump(DModel m, DState st, int env, const
     out[DUMP_EFC + 3 * MAXEFC + r] = v ? (float)s.efc_type[r] : -1.f;
   }
 }
-
-#endif  // !AW_WIDE
 
 #ifndef AW_TASK_TU   // task-independent kernels: in the API translation unit only
 __global__ void __launch_bounds__(64) k_task_eval(DModel m, int n, const float* qpos, const float* qvel,
@@ -1111,6 +1217,8 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
   m.tar_length = (float)B.opt("task_tar_length", 1);
   m.task_kind = B.dim("task_kind"); m.frame_skip = B.dim("task_frame_skip", 1);
   m.horizon = B.dim("task_horizon", 0); m.obs_dim = B.dim("task_obs_dim", 0);
+  // the observation is assembled in the row buffer (write_obs): it must fit the fast tier's
+  if (m.obs_dim < 0 || m.obs_dim > 64 * FAST_NRL) return fail(AW_EUNSUPPORTED, "observation larger than the row buffer");
   m.success_steps = B.dim("task_success_steps", 25);
   m.nparam = B.dim("task_nparam", 0); m.variation = B.dim("task_variation", 0);
   if (m.nparam > MAXP) return fail(AW_EUNSUPPORTED, "too many per-env params");
@@ -1403,6 +1511,7 @@ static int build_model(const Blob& B, DModel& m, MData& md) {
 struct WideOps {
   int (*slots)(int device);
   void (*run)(aw_handle*, const float*, float*, float*, uint8_t*, uint8_t*, float*, int, uint64_t, hipStream_t);
+  void (*dump)(aw_handle*, int, const float*, float*, hipStream_t);   // aw_forward_dump_wide
 };
 template <int TASK> const WideOps* wide_ops();
 
@@ -1418,10 +1527,16 @@ template <int TASK>
 static void launch_wide(aw_handle* h, const float* a, float* obs, float* rew, uint8_t* done, uint8_t* goal,
                         float* tobs, int autoreset, uint64_t seed, hipStream_t st) {
   hipLaunchKernelGGL((k_step_wide<TASK>), dim3(h->wide_grid), dim3(64), 0, st, (const DModel*)h->dmhdr_wide, a, obs, rew,
-                     done, goal, tobs, autoreset, seed, h->next_env + 8);
+                     done, goal, tobs, autoreset, seed, h->next_env + 8, h->nenv);
+}
+template <int TASK>
+static void launch_dump_wide(aw_handle* h, int env, const float* ctrl, float* out, hipStream_t st) {
+  DModel mw = h->m;
+  mw.jspill = h->jspill_wide;   // the dense rows past JL in the wide tier's spill block (slot 0)
+  hipLaunchKernelGGL((k_dump_wide<TASK>), dim3(1), dim3(64), 0, st, mw, h->st, env, ctrl, out);
 }
 template <int TASK> const WideOps* wide_ops() {
-  static const WideOps ops = {wide_slots<TASK>, launch_wide<TASK>};
+  static const WideOps ops = {wide_slots<TASK>, launch_wide<TASK>, launch_dump_wide<TASK>};
   return &ops;
 }
 template const WideOps* wide_ops<AW_TASK_TU>();
@@ -1901,6 +2016,16 @@ int aw_forward_dump(aw_handle* h, int env, const float* ctrl, float* out, void* 
   if (!h || !out || env < 0 || env >= h->nenv) return fail(AW_EINVAL, "aw_forward_dump: bad arguments");
   HIPCHK(hipSetDevice(h->device));
 #define CALL(TT) task_ops<TT>()->dump(h, env, ctrl, out, (hipStream_t)stream)
+  DISPATCH_TASK(h->m.task_kind, CALL)
+#undef CALL
+  HIPCHK(hipGetLastError());
+  return AW_OK;
+}
+
+int aw_forward_dump_wide(aw_handle* h, int env, const float* ctrl, float* out, void* stream) {
+  if (!h || !out || env < 0 || env >= h->nenv) return fail(AW_EINVAL, "aw_forward_dump_wide: bad arguments");
+  HIPCHK(hipSetDevice(h->device));
+#define CALL(TT) wide_ops<TT>()->dump(h, env, ctrl, out, (hipStream_t)stream)
   DISPATCH_TASK(h->m.task_kind, CALL)
 #undef CALL
   HIPCHK(hipGetLastError());

@@ -73,12 +73,16 @@ constexpr int FAST_MAXCON = 48, FAST_NRL = 3, FAST_MAXDENSE = AW_FAST_MD;
 static_assert(FAST_MAXDENSE <= FAST_MAXDENSE_ALLOC, "fast spill blocks are allocated for FAST_MAXDENSE_ALLOC");
 #define AW_CAT2(a, b) a##b
 #define AW_CAT(a, b) AW_CAT2(a, b)
-constexpr int WIDE_MAXCON = 100, WIDE_NRL = 8, WIDE_MAXDENSE = 500;
+// the wide tier STORES up to 128 raw contacts (two 64-lane chunks) and keeps MuJoCo's nconmax of them:
+// the near-margin candidates the fp64 decision drops (aw_collide.h DEC_EPS) never cost a real contact
+// its slot, and past nconmax the kept ones are the first 100 in pair order, as mj_collision keeps them
+constexpr int WIDE_MAXCON = 128, WIDE_NRL = 8, WIDE_MAXDENSE = 500;
 constexpr int NCONMAX = 100, NJMAX = 500;   // the reference model's caps (DAPG_assets.xml:4)
 #ifdef AW_WIDE
 inline namespace wide {
 constexpr bool WIDE = true;
-constexpr int MAXCON = WIDE_MAXCON;   // contacts per env (64 per chunk in the lane-per-contact stages)
+constexpr int MAXCON = WIDE_MAXCON;   // contacts stored per env (64 per chunk in the lane-per-contact stages)
+constexpr int CON_CAP = NCONMAX;      // contacts kept: MuJoCo's nconmax (DAPG_assets.xml:4)
 constexpr int NRL = WIDE_NRL;         // constraint rows per lane in the Newton solver
 constexpr int EFC_CAP = NJMAX;        // rows kept (MuJoCo's njmax), storage MAXEFC >= EFC_CAP
 constexpr int MAXDENSE = WIDE_MAXDENSE;
@@ -86,11 +90,13 @@ constexpr int MAXDENSE = WIDE_MAXDENSE;
 inline namespace AW_CAT(fast, AW_FAST_MD) {   // fast128 / fast192
 constexpr bool WIDE = false;
 constexpr int MAXCON = FAST_MAXCON;   // contacts per env (one lane each in the sort)
+constexpr int CON_CAP = FAST_MAXCON;  // a raw candidate past the storage defers the env-step to the wide tier
 constexpr int NRL = FAST_NRL;         // constraint rows per lane in the Newton solver
 constexpr int EFC_CAP = 64 * FAST_NRL;
 constexpr int MAXDENSE = FAST_MAXDENSE;  // dense (contact) rows
 #endif
 constexpr int MAXEFC = 64 * NRL;      // constraint rows (fast 192, wide 512)
+static_assert(CON_CAP <= MAXCON, "contact storage");
 constexpr int NCH = (MAXCON + 63) / 64;      // 64-contact chunks of the lane-per-contact stages
 constexpr int NDCH = (MAXDENSE + 63) / 64;   // 64-row chunks of the dense rows (noslip pair scan)
 constexpr int JL = 32;        // dense J rows kept in LDS; rows [JL, MAXDENSE) live in the env's global

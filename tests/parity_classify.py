@@ -121,11 +121,11 @@ class Ctx:
         return self.torch.tensor(np.asarray(a), dtype=self.torch.float32, device="cuda")
 
     # --- one forward on each side from an identical state --------------------------------------
-    def gpu_forward(self, params, q, v, w, ctrl, disableflags=0):
+    def gpu_forward(self, params, q, v, w, ctrl, disableflags=0, wide=False):
         if disableflags:
             self.one.set_option(disableflags=disableflags)
         self.one.set_state(self._t(q[None]), self._t(v[None]), self._t(w[None]), self._t(np.asarray(params)[None]))
-        d = self.one.forward_dump(0, self._t(ctrl))
+        d = self.one.forward_dump(0, self._t(ctrl), wide=wide)
         if disableflags:
             self.one.set_option(disableflags=0)
         return d
@@ -454,6 +454,49 @@ def shadowed(ctx, params, qpos, qvel, warm, act, gpu, jar_log=None):
     if same:
         return "shadowed", f"local substep errors <= {worst:.3f} of the tolerance"
     return None, "the substep replay does not end on the env-step result"
+
+
+def newton_cost(M, a0, J, aref, D, fl, ty, a):
+    """mj_solNewton's objective at qacc a, in fp64: the Gauss term 1/2 (a - a0)' M (a - a0) plus each
+    row's piecewise-quadratic cost (frictionloss rows: quadratic within +-R floss, linear beyond;
+    contact / limit rows: quadratic when jar < 0)"""
+    d = np.asarray(a, float) - a0
+    c = 0.5 * d @ M @ d
+    jar = J @ a - aref
+    R = 1.0 / D
+    for r in range(len(jar)):
+        x = jar[r]
+        if ty[r] <= 1:
+            f = fl[r]
+            if x <= -R[r] * f:
+                c += -f * x - 0.5 * R[r] * f * f
+            elif x >= R[r] * f:
+                c += f * x - 0.5 * R[r] * f * f
+            else:
+                c += 0.5 * D[r] * x * x
+        elif x < 0:
+            c += 0.5 * D[r] * x * x
+    return c
+
+
+def newton_gap(ctx, params, q, v, w, ctrl, wide=False):
+    """The GPU's Newton solution (noslip off) in the REFERENCE's own problem: (objective at the oracle's
+    qacc, at the GPU's, at qacc_smooth) from the identical fp32 state, and the two dumps"""
+    q, v, w = f32(q), f32(v), f32(w)
+    dn = ctx.gpu_forward(params, q, v, w, ctrl, disableflags=DSBL_NOSLIP, wide=wide)
+    o = ctx.o
+    o.set_option(disableflags=DSBL_NOSLIP)
+    o.forward1(params, q, v, w, ctrl)
+    nv = len(o.get("qacc"))
+    M, a0, qa = o.get("qM").reshape(nv, nv), o.get("qacc_smooth"), o.get("qacc")
+    J = o.get("efc_J").reshape(-1, nv)
+    aref, D, fl, ty = o.get("efc_aref"), o.get("efc_D"), o.get("efc_frictionloss"), o.get("efc_type").astype(int)
+    sc = o.get("scalars")
+    o.set_option(disableflags=0)
+    args = (M, a0, J, aref, D, fl, ty)
+    return dict(c_oracle=newton_cost(*args, qa), c_gpu=newton_cost(*args, dn["qacc"]), c_smooth=newton_cost(*args, a0),
+                gpu=dn, oracle_qacc=qa, oracle_qacc_smooth=a0, oracle_ncon=int(sc[0]), oracle_nefc=int(sc[1]),
+                oracle_iter=int(sc[2]))
 
 
 _ORACLE_F32 = {}

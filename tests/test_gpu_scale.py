@@ -305,3 +305,65 @@ def test_dapg_teacher_forced_config3_size(env_id):
     assert not unexplained, unexplained
     _err_gate(err)
 
+
+
+# --------------------------------------------------------------------------------------------
+def test_wide_tier_high_contact_forward_vs_oracle():
+    """The wide tier past the fast capacities against the oracle (advisor r05): a test-only model with
+    every geom margin at 0.08 m (conftest "margin=" pseudo-variation) puts hammer-v0 at 60-80 contacts,
+    ~400 rows and ~370 dense rows -- the second 64-contact chunk of sort_contacts / the row assembly /
+    stage_touch, the chunked dense-row offsets, 8 rows per lane in Newton and the L2 spill rows past
+    JL.  aw_forward_dump_wide runs one forward of such states through the wide tier; the oracle runs
+    the same fp32 state at MuJoCo's nconmax 100 / njmax 500.  Compared: every geom pair's contact list
+    (a pair whose list differs must be a tie the reference itself flips under 16-ulp inputs), the row
+    types, qacc_smooth, and the wide Newton's solution (noslip off) priced in the REFERENCE's objective:
+    its optimality gap relative to the solve's decrease."""
+    from mj_envs_amd.tasks import sample_params
+    from parity_classify import (_contacts, _lists_differ, _unmatched, context, f32, newton_gap, oracle_tie)
+    env_id, var = "hammer-v0", "margin=0.08"
+    ctx = context(env_id, var)
+    o = ctx.o
+    n = 32
+    rng = np.random.default_rng(61)
+    P = f32(sample_params(env_id, ctx.m, rng, n))
+    st, _ = o.reset(P)
+    states = []
+    for k in range(8):
+        a = f32(rng.uniform(-1, 1, (n, o.nu)))
+        o.step(st, a, nthreads=8)
+        if k >= 3:
+            states += [(P[e], f32(st["qpos"][e]), f32(st["qvel"][e]), f32(st["warm"][e]), ctx.ctrl(a[e])) for e in range(n)]
+    big = dict(ncon=0, nefc=0, ndense=0)
+    gaps, n_cmp, n_tie = [], 0, 0
+    for params, q, v, w, ctrl in states:
+        d = ctx.gpu_forward(params, q, v, w, ctrl, wide=True)
+        o.forward1(params, q, v, w, ctrl)
+        sc = o.get("scalars")
+        if int(sc[0]) <= 64:
+            continue
+        assert not (d["status"] & 24), "the wide tier dropped a constraint below MuJoCo's caps"
+        big = {k: max(big[k], d[k]) for k in big}
+        gc, oc = _contacts(ctx, d, o.get("contact").reshape(-1, 23))
+        ties = [key for key in dict.fromkeys(list(gc) + list(oc))
+                if _lists_differ(gc.get(key, []), oc.get(key, [])) or any(_unmatched(gc.get(key, []), oc.get(key, [])))]
+        for key in ties:
+            assert oracle_tie(ctx, key, params, q, v, w, ctrl), \
+                f"pair {ctx.gname(key[0])}|{ctx.gname(key[1])}: contacts differ and the reference's are stable"
+        n_tie += bool(ties)
+        np.testing.assert_allclose(d["qacc_smooth"], o.get("qacc_smooth"), rtol=1e-3,
+                                   atol=1e-4 * np.abs(o.get("qacc_smooth")).max())
+        if ties:
+            continue
+        n_cmp += 1
+        assert d["nefc"] == int(sc[1])
+        np.testing.assert_array_equal(d["efc_type"], o.get("efc_type"))
+        np.testing.assert_allclose(d["efc_D"], o.get("efc_D"), rtol=2e-3)
+        g = newton_gap(ctx, params, q, v, w, ctrl, wide=True)
+        gaps.append((g["c_gpu"] - g["c_oracle"]) / max(g["c_smooth"] - g["c_oracle"], 1e-30))
+    gaps = np.array(gaps)
+    print(f"wide tier, margin 0.08: {n_cmp} states compared row by row, {n_tie} with a collider tie; max ncon "
+          f"{big['ncon']}, nefc {big['nefc']}, dense rows {big['ndense']}; Newton optimality gap in the reference's "
+          f"objective (relative to the solve's decrease) p50 {np.median(gaps):.1e} max {gaps.max():.1e}")
+    assert big["ncon"] > 64 and big["nefc"] > 192 and big["ndense"] > 128, big
+    assert n_cmp >= 8
+    assert np.median(gaps) < 1e-4 and gaps.max() < 1e-2, gaps
