@@ -114,12 +114,14 @@ def _oracle_f32_model(m):
     return Oracle(m.to_blob())
 
 
-def _miss_is_fp32_sensitive(o, o32, st, act, gpu=None, trials=8, ulps=16, seed=0, factor=4.0):
-    """tests/test_gpu_parity.py _fp32_sensitive: the oracle's own env-step leaves the one-step
+def _miss_is_fp32_sensitive(o, o32, st, act, gpu=None, trials=8, ulps=16, seed=0, factor=4.0, ratio_out=None):
+    """tests/parity_classify.py fp32_sensitive: the oracle's own env-step leaves the one-step
     tolerance when re-run on the fp32-rounded model or from the state perturbed by <= 16 fp32 ulps
     per component -- the step is on a switch / ill-conditioned at fp32 resolution -- AND (given the
     GPU's post-step state gpu = (qpos, qvel)) the GPU's deviation from the unperturbed fp64 result
-    is within `factor` x the largest deviation of those runs (or within tolerance), in qpos and qvel"""
+    is within `factor` x the largest deviation of those runs (or within tolerance), in qpos and qvel.
+    ratio_out (a list) receives the GPU's deviation / the runs' spread (0 where within tolerance),
+    so a drift towards `factor` stays visible (advisor r05)"""
     import numpy as np
     rng = np.random.default_rng(seed)
     base = {k: v.copy() for k, v in st.items()}
@@ -143,9 +145,12 @@ def _miss_is_fp32_sensitive(o, o32, st, act, gpu=None, trials=8, ulps=16, seed=0
     if not leaves or gpu is None:
         return leaves
     gq, gv = np.asarray(gpu[0], float).reshape(bq.shape), np.asarray(gpu[1], float).reshape(bv.shape)
-    okq = tolq(gq) or float(np.abs(gq - bq).max()) <= factor * dq
-    okv = tolv(gv) or float((np.abs(gv - bv) / (1 + np.abs(bv))).max()) <= factor * dv
-    return bool(okq and okv)
+    eq, ev = float(np.abs(gq - bq).max()), float((np.abs(gv - bv) / (1 + np.abs(bv))).max())
+    rq = 0.0 if tolq(gq) else (eq / dq if dq > 0 else float("inf"))
+    rv = 0.0 if tolv(gv) else (ev / dv if dv > 0 else float("inf"))
+    if ratio_out is not None:
+        ratio_out.append(max(rq, rv))
+    return bool(rq <= factor and rv <= factor)
 
 
 def same_run_parity(blob, sim, n=256, model=None, pol=None, obs_now=None):
@@ -185,14 +190,14 @@ def same_run_parity(blob, sim, n=256, model=None, pol=None, obs_now=None):
     # every miss re-checked as the parity tests do: is the fp64 reference itself unstable at fp32
     # resolution there, with the GPU inside that instability (tests/test_gpu_parity.py
     # _classify_misses, criterion b)?  All misses are classified.
-    sens = []
+    sens, ratios = [], []
     miss_idx = np.nonzero(~ok)[0]
     if model is not None and miss_idx.size:
         o32 = _oracle_f32_model(model)
         for k in miss_idx:
             stk = {key: st0[key][k:k + 1].copy() for key in st0}
             sens.append(bool(_miss_is_fp32_sensitive(o, o32, stk, g(act)[k:k + 1],
-                                                     gpu=(qg[k:k + 1], vg[k:k + 1]))))
+                                                     gpu=(qg[k:k + 1], vg[k:k + 1]), ratio_out=ratios)))
     eq = np.abs(qg - st["qpos"]).max(axis=1)
     ev = (np.abs(vg - st["qvel"]) / (1 + np.abs(st["qvel"]))).max(axis=1)
     return dict(envs=len(idx), handle_envs=N, grid=sim.grid, sampled="evenly over the whole batch (incl. "
@@ -201,6 +206,7 @@ def same_run_parity(blob, sim, n=256, model=None, pol=None, obs_now=None):
                 misses_classified=len(sens) if model is not None else 0,
                 misses_fp32_sensitive_reference=sum(sens), misses_unexplained=len(sens) - sum(sens)
                 if model is not None else None,
+                miss_spread_ratios=[round(r, 3) for r in ratios], max_spread_ratio=max(ratios) if ratios else None,
                 max_abs_qpos=float(eq.max()), max_rel_qvel=float(ev.max()),
                 p50_abs_qpos=float(np.median(eq)), p99_abs_qpos=float(np.percentile(eq, 99)),
                 median_abs_obs=float(np.median(np.abs(obs.cpu().numpy()[idx] - o_obs))),
