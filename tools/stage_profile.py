@@ -19,13 +19,13 @@ PROF_LIB = os.path.join(REPO, "mj_envs_amd", "libadroit_hip_prof.so")
 def build(task: int = 0):
     """one-TU profiling build of the fast tier + the task's wide-tier object (no markers there)"""
     sys.path.insert(0, REPO)
-    from __graft_entry__ import HIPCC_FLAGS, compile_units, wide_unit
+    from __graft_entry__ import HIPCC_FLAGS, compile_units, hipcc_path, wide_unit
     objdir = os.path.join(REPO, "build", "hip")
     os.makedirs(objdir, exist_ok=True)
     prof_o = os.path.join(objdir, "prof_fast.o")
     units = [(f"-DAW_STAGE_PROF -DAW_ONLY_TASK={task}", prof_o), wide_unit(task, objdir, "prof")]
     compile_units(units)
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", PROF_LIB,
+    subprocess.run([hipcc_path(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", PROF_LIB,
                     *[u[1] for u in units]], check=True)
 
 
