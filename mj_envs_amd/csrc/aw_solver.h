@@ -1089,9 +1089,21 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
         if (4 * q + t < NV) Am[4 * q + t] = vv[t];
     }
   }
+  // With >= 4 pair lanes (NPL <= 32) the pair-pair block G is formed on the matrix cores below; its
+  // diagonal is K = jd_q . xd_q and one extra B column (qacc, at index npl) gives S = jd_q . qacc, so
+  // the pair lanes' own difference rows (per-lane Jacobian rows: 8-way LDS bank conflicts) are not read
+  // at all (AW_NS_KS_MFMA; the same products in the same k order as the VALU chains below)
+#ifndef AW_NS_KS_MFMA
+#define AW_NS_KS_MFMA 0
+#endif
+  const bool g_mfma_ks = AW_NS_KS_MFMA && NPL <= 32 && npl >= 4;
+  if (pl) {
+    fa = s.efc_force[nsparse + rowe];
+    fb = s.efc_force[nsparse + rowe + 1];
+  }
   // pair lanes: their difference row jd_q (registers), K = jd_q . xd_q, jd_q . qacc and constants
   float jq[NV];
-  {
+  if (!g_mfma_ks) {
     const int e = pl ? rowe : 0;
     if (e + 1 < JL) {
 #pragma unroll
@@ -1118,8 +1130,6 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
       ca = ok ? 1.0f / K : 0.f;
       cb = (s.efc_aref[nsparse + e] - s.efc_aref[nsparse + e + 1]) * ca;
       diag = ok ? K : 0.f;
-      fa = s.efc_force[nsparse + e];
-      fb = s.efc_force[nsparse + e + 1];
       R = S;
     }
   }
@@ -1144,7 +1154,8 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
         for (int p = 0; p < NPL; p++)
           if (p < npl) Ap[p] = Xb[p * XS + li];
         const int sub = lane >> 4, col = lane & 15;
-        const bool two = npl > 16;
+        const int ncol = g_mfma_ks ? npl + 1 : npl;   // + the qacc column (S)
+        const bool two = ncol > 16;
         const float* r0[2];
         const float* r1[2];
         bool qv[2], pv[2];
@@ -1170,6 +1181,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
           for (int t = 0; t < 2; t++) {
             a[t] = (kv && qv[t]) ? r0[t][kk] - r1[t][kk] : 0.f;
             b[t] = (kv && pv[t]) ? Xb[(16 * t + col) * XS + kk] : 0.f;
+            if (g_mfma_ks && 16 * t + col == npl) b[t] = kv ? s.rowbuf[kk] : 0.f;   // qacc (rowbuf, above)
           }
           c00 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c00, 0, 0, 0);
           if (two) {
@@ -1200,6 +1212,14 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
 #pragma unroll
             for (int t = 0; t < 4; t++)
               if (4 * q + t < NPL) Ap[4 * q + t] = vv[t];
+          }
+          if (g_mfma_ks) {
+            const float K = gr[lane - NV], S = gr[npl];
+            const bool ok = K >= MINVAL;
+            ca = ok ? 1.0f / K : 0.f;
+            cb = (s.efc_aref[nsparse + rowe] - s.efc_aref[nsparse + rowe + 1]) * ca;
+            diag = ok ? K : 0.f;
+            R = S;
           }
         }
         wsync();
