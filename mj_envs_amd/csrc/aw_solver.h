@@ -493,20 +493,48 @@ constexpr float NT_NOISE_DOF = AW_NT_NOISE_DOF;
 // NT_EXIT_NOROWS: no constraint rows, no Newton solve (forward's default before the solver runs)
 enum { NT_EXIT_MAXITER = 0, NT_EXIT_NOSTEP = 1, NT_EXIT_NOISE = 2, NT_EXIT_IMPROVE = 3, NT_EXIT_GRAD = 4, NT_EXIT_NOROWS = 5 };
 struct RowR {
-  float D, floss, Jaref, Jp, force;
+  float D, R, floss, Jaref, Jp, force;   // R = 1 / D (the regularisation), formed once per solve
   int st, fr, valid;
 };
 
+// mj_solNewton's row cost, force and state at jar.  Branch-free (AW_ROW_EVAL_SELECT, default): every
+// zone's value is formed with the same expressions as the branching form and the row's zone selects
+// one -- the branching form compiled to four levels of divergent exec-mask regions per row, on every
+// line-search derivative (three rows per lane) and cost evaluation.  Bitwise the same results.
+#ifndef AW_ROW_EVAL_SELECT
+#define AW_ROW_EVAL_SELECT 1
+#endif
 AW_DEV float row_eval(const RowR& r, float jar, float* force, int* st) {
+#if AW_ROW_EVAL_SELECT
+  const float f = r.floss, R = r.R;
+  const float fq = -r.D * jar, cq = 0.5f * r.D * jar * jar;          // quadratic zone
+  const float cn = -f * jar - 0.5f * R * f * f, cp = f * jar - 0.5f * R * f * f;   // linear zones
+  const bool neg = jar <= -R * f, pos = jar >= R * f, quad = jar < 0;
+  float fo, c;
+  int so;
+  if (r.fr) {   // uniform per row slot (a select, not a branch, in the unrolled row loops)
+    fo = neg ? f : (pos ? -f : fq);
+    c = neg ? cn : (pos ? cp : cq);
+    so = neg ? S_LNEG : (pos ? S_LPOS : S_QUAD);
+  } else {
+    fo = quad ? fq : 0.f;
+    c = quad ? cq : 0.f;
+    so = quad ? S_QUAD : S_SAT;
+  }
+  *force = r.valid ? fo : 0.f;
+  *st = r.valid ? so : S_SAT;
+  return r.valid ? c : 0.f;
+#else
   if (!r.valid) { *force = 0.f; *st = S_SAT; return 0.f; }
   if (r.fr) {
-    float f = r.floss, R = 1.f / r.D;
+    float f = r.floss, R = r.R;
     if (jar <= -R * f) { *force = f; *st = S_LNEG; return -f * jar - 0.5f * R * f * f; }
     if (jar >= R * f) { *force = -f; *st = S_LPOS; return f * jar - 0.5f * R * f * f; }
     *force = -r.D * jar; *st = S_QUAD; return 0.5f * r.D * jar * jar;
   }
   if (jar < 0) { *force = -r.D * jar; *st = S_QUAD; return 0.5f * r.D * jar * jar; }
   *force = 0.f; *st = S_SAT; return 0.f;
+#endif
 }
 
 // J_d' diag(w) J_d over the dense rows (weights w_d in s.rowbuf[nsparse + d], 0 for rows outside
@@ -595,6 +623,7 @@ AW_DEV void solve_newton(const DModel& m, Env& s, int lane_nt, const float (&Mro
     rr[h].valid = r < nefc;
     int rc = rr[h].valid ? r : 0;
     rr[h].D = s.efc_D[rc];
+    rr[h].R = 1.f / rr[h].D;
     rr[h].floss = s.efc_floss[rc];
     int t = s.efc_type[rc];
     rr[h].fr = (t == C_FRIC_DOF || t == C_FRIC_TEN);
@@ -1094,7 +1123,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
   // the pair lanes' own difference rows (per-lane Jacobian rows: 8-way LDS bank conflicts) are not read
   // at all (AW_NS_KS_MFMA; the same products in the same k order as the VALU chains below)
 #ifndef AW_NS_KS_MFMA
-#define AW_NS_KS_MFMA 0
+#define AW_NS_KS_MFMA 1
 #endif
   const bool g_mfma_ks = AW_NS_KS_MFMA && NPL <= 32 && npl >= 4;
   if (pl) {
