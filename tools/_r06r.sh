@@ -1,14 +1,19 @@
 set -e
-timeout -k 10 120 python -u tools/rollout_dump.py /tmp/r06r_main.npz > gpurun_out/r06r_dump.log 2>&1
-AW_LIB=mj_envs_amd/libadroit_hip_rsel0.so timeout -k 10 120 python -u tools/rollout_dump.py /tmp/r06r_rsel0.npz >> gpurun_out/r06r_dump.log 2>&1
-AW_LIB=mj_envs_amd/libadroit_hip_kson.so timeout -k 10 120 python -u tools/rollout_dump.py /tmp/r06r_kson.npz >> gpurun_out/r06r_dump.log 2>&1
-python - >> gpurun_out/r06r_dump.log <<'PY'
+# usage: bash tools/_r06r.sh TAG variant...   (bitwise rollouts of each variant against main, then A/B)
+TAG=$1; shift
+timeout -k 10 120 python -u tools/rollout_dump.py /tmp/${TAG}_main.npz > gpurun_out/${TAG}_dump.log 2>&1
+for v in "$@"; do
+  AW_LIB=mj_envs_amd/libadroit_hip_$v.so timeout -k 10 120 python -u tools/rollout_dump.py /tmp/${TAG}_$v.npz >> gpurun_out/${TAG}_dump.log 2>&1
+done
+python - "$TAG" "$@" >> gpurun_out/${TAG}_dump.log <<'PY'
+import sys
 import numpy as np
-a = np.load("/tmp/r06r_main.npz")
-for other in ("rsel0", "kson"):
-    b = np.load(f"/tmp/r06r_{other}.npz")
+tag = sys.argv[1]
+a = np.load(f"/tmp/{tag}_main.npz")
+for other in sys.argv[2:]:
+    b = np.load(f"/tmp/{tag}_{other}.npz")
     for k in a.files:
         print("main vs", other, k, "bitwise equal" if np.array_equal(a[k], b[k]) else f"DIFFER max {np.abs(a[k]-b[k]).max():.3e}")
 PY
-bash tools/ab.sh rsel0 main kson > gpurun_out/r06r_ab_random.txt 2>&1
-bash tools/ab.sh -p dapg rsel0 main kson > gpurun_out/r06r_ab_dapg.txt 2>&1
+bash tools/ab.sh main "$@" > gpurun_out/${TAG}_ab_random.txt 2>&1
+bash tools/ab.sh -p dapg main "$@" > gpurun_out/${TAG}_ab_dapg.txt 2>&1
