@@ -420,8 +420,9 @@ AW_DEV void stage_crb(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
         const int i = 16 * t + col;
         const bool v = cv && i < NV;
         const int ii = i < NV ? i : NV - 1;
-        a[t] = v ? s.buf[ii][cc] : 0.f;
-        b[t] = v ? s.cdof[ii][cc] : 0.f;
+        const float av = s.buf[ii][cc], bv = s.cdof[ii][cc];   // valid (ii, cc): load, then select
+        a[t] = v ? av : 0.f;
+        b[t] = v ? bv : 0.f;
       }
 #pragma unroll
       for (int ti = 0; ti < NT; ti++)
@@ -452,7 +453,7 @@ AW_DEV void stage_crb(const DModel& m, Env& s, int lane, float (&Mrow)[NV]) {
       for (int t = 0; t < 4; t++) {
         const int k = 4 * q + t;
         if (k >= NV) continue;
-        const bool rel = ((anc >> k) & 1ull) || ((MD(dof_ancmask, k) >> li) & 1ull);
+        const bool rel = ((anc >> k) | (MD(dof_ancmask, k) >> li)) & 1ull;   // no short-circuit branch
         Mrow[k] = k == li ? vv[t] + arm : (rel ? vv[t] : 0.f);
       }
     }

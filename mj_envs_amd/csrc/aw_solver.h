@@ -162,8 +162,9 @@ AW_DEV void jspill_fence() {
 template <int NV>
 AW_DEV float row_dot(const DModel& m, const Env& s, int r, const float* x) {
   if (r < s.nsparse) {
-    int i1 = s.efc_i1[r];
-    return s.efc_v0[r] * x[s.efc_i0[r]] + (i1 >= 0 ? s.efc_v1[r] * x[i1] : 0.f);
+    const int i1 = s.efc_i1[r];
+    const float x1 = x[i1 >= 0 ? i1 : 0], v1 = s.efc_v1[r];   // loaded unconditionally, then selected
+    return s.efc_v0[r] * x[s.efc_i0[r]] + (i1 >= 0 ? v1 * x1 : 0.f);
   }
   const int d = r - s.nsparse;
   float acc = 0.f;
@@ -185,8 +186,10 @@ AW_DEV void row_dot2(const DModel& m, const Env& s, int r, const float* x, const
   if (r < s.nsparse) {
     const int i0 = s.efc_i0[r], i1 = s.efc_i1[r];
     const float v0 = s.efc_v0[r], v1 = s.efc_v1[r];
-    dx = v0 * x[i0] + (i1 >= 0 ? v1 * x[i1] : 0.f);
-    dy = v0 * y[i0] + (i1 >= 0 ? v1 * y[i1] : 0.f);
+    const int j1 = i1 >= 0 ? i1 : 0;   // loaded unconditionally, then selected
+    const float x1 = x[j1], y1 = y[j1];
+    dx = v0 * x[i0] + (i1 >= 0 ? v1 * x1 : 0.f);
+    dy = v0 * y[i0] + (i1 >= 0 ? v1 * y1 : 0.f);
     return;
   }
   const int d = r - s.nsparse;
@@ -512,7 +515,7 @@ AW_DEV float row_eval(const RowR& r, float jar, float* force, int* st) {
   const bool neg = jar <= -R * f, pos = jar >= R * f, quad = jar < 0;
   float fo, c;
   int so;
-  if (r.fr) {   // uniform per row slot (a select, not a branch, in the unrolled row loops)
+  if (r.fr) {   // a branch on the row type: a slot whose lanes are all contact rows skips this side
     fo = neg ? f : (pos ? -f : fq);
     c = neg ? cn : (pos ? cp : cq);
     so = neg ? S_LNEG : (pos ? S_LPOS : S_QUAD);
@@ -562,7 +565,8 @@ AW_DEV void hess_dense_mfma(const DModel& m, Env& s, int lane) {
     const int dd = v ? d : d0;   // a row of this K-step (d0 < nd): in the same storage as the rest
     // JL is a multiple of 4: a K-step's rows are all in LDS or all in the spill block
     const float* Jr = d0 < JL ? &s.J[dd][0] : (const float*)jspill_row(m, s, dd);
-    w = v ? s.rowbuf[ns + dd] : 0.f;
+    const float wl = s.rowbuf[ns + dd];   // dd is a row of this K-step: loaded unconditionally, then
+    w = v ? wl : 0.f;                     // selected (a conditional load is an exec-mask branch)
     b0 = Jr[col];
     b1 = Jr[16 + col];
     b1 = 16 + col < NV ? b1 : 0.f;
@@ -1077,10 +1081,14 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
 #pragma unroll
         for (int ti = 0; ti < NTI; ti++) {
           const int i = 16 * ti + col;
-          a[ti] = (kv && i < NV) ? Xb[(i < NV ? i : 0) * XS + kk] : 0.f;
+          const float xv = Xb[(i < NV ? i : 0) * XS + kk];
+          a[ti] = (kv && i < NV) ? xv : 0.f;
         }
 #pragma unroll
-        for (int t = 0; t < 2; t++) b[t] = (kv && pv[t]) ? r0[t][kk] - r1[t][kk] : 0.f;
+        for (int t = 0; t < 2; t++) {
+          const float jv = r0[t][kk] - r1[t][kk];   // valid rows (e = 0 / kk = 0 stand-ins)
+          b[t] = (kv && pv[t]) ? jv : 0.f;
+        }
 #pragma unroll
         for (int ti = 0; ti < NTI; ti++) {
           c[ti][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ti], b[0], c[ti][0], 0, 0, 0);
@@ -1180,8 +1188,7 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
         g_mfma = true;
         typedef float f4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-        for (int p = 0; p < NPL; p++)
-          if (p < npl) Ap[p] = Xb[p * XS + li];
+        for (int p = 0; p < NPL; p++) Ap[p] = Xb[p * XS + li];   // entries p >= npl are never read
         const int sub = lane >> 4, col = lane & 15;
         const int ncol = g_mfma_ks ? npl + 1 : npl;   // + the qacc column (S)
         const bool two = ncol > 16;
@@ -1208,9 +1215,13 @@ AW_DEV void solve_noslip(const DModel& m, Env& s, int lane_ns, const float (&Mro
           float a[2], b[2];
 #pragma unroll
           for (int t = 0; t < 2; t++) {
-            a[t] = (kv && qv[t]) ? r0[t][kk] - r1[t][kk] : 0.f;
-            b[t] = (kv && pv[t]) ? Xb[(16 * t + col) * XS + kk] : 0.f;
-            if (g_mfma_ks && 16 * t + col == npl) b[t] = kv ? s.rowbuf[kk] : 0.f;   // qacc (rowbuf, above)
+            // operands read from valid addresses (stand-in row 0 / column 0), then selected; the
+            // compiler still sinks some reads under the lane conditions, which measured faster than
+            // forcing them all (r06v: +0.8 % DAPG with the reads pinned)
+            const float jv = r0[t][kk] - r1[t][kk], xv = Xb[(16 * t + col) * XS + kk], qa = s.rowbuf[kk];
+            a[t] = (kv && qv[t]) ? jv : 0.f;
+            b[t] = (kv && pv[t]) ? xv : 0.f;
+            if (g_mfma_ks && 16 * t + col == npl) b[t] = kv ? qa : 0.f;   // qacc (rowbuf, above)
           }
           c00 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c00, 0, 0, 0);
           if (two) {
