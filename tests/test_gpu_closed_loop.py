@@ -285,23 +285,69 @@ def test_nan_state_flags_and_resets_like_oracle(field):
 
 
 # --------------------------------------------------------------------------------------------
+# steps of the config-4 run at which sampled envs are teacher-forced against the oracle
+C4_CHECK = (0, 50, 100, 150, 205)
+
+
 def test_config4_262144_envs_one_gpu_properties():
-    """BASELINE config 4 (hammer, 262 144 envs; 8 x 32 768 per GPU) on one GPU: the shard of
-    rank r is envs [32 768 r, 32 768 (r + 1)) of the batch, so one 262 144-env handle and the
-    rank-3 shard (offset 98 304) must agree bit for bit on those envs; all outputs finite."""
-    env_id, n, per = "hammer-v0", 262144, 32768
+    """BASELINE config 4 (hammer, 262 144 envs; 8 x 32 768 per GPU) on one GPU over 210 env-steps,
+    across the horizon-200 auto-reset: the rank-3 shard (offset 98 304) agrees bit for bit with the
+    262 144-env handle on its envs at EVERY step (obs, reward, done); all outputs finite; no env drops
+    a constraint MuJoCo keeps; and at five steps 64 envs sampled across the whole batch are
+    teacher-forced against the oracle (one-step tolerance, misses classified)."""
+    from mj_envs_amd import _native
+    from test_gpu_parity import ONE_STEP_MIN, _classify_misses, _hard_cap, _state_err
+    env_id, n, per, steps = "hammer-v0", 262144, 32768, 210
+    _, o = make_oracle(env_id)
     _, full = _sim(env_id, n)
     _, shard = _sim(env_id, per, env_offset=3 * per)
-    res = []
-    for s in (full, shard):
-        obs, rew, done, goal = _bufs(s, s.n_envs)
-        act = s.empty(s.n_envs, s.nu)
-        s.reset(obs, seed=4)
-        for k in range(3):
-            s.random_actions(act, 9, k)
-            s.step(act, obs, rew, done, goal, autoreset=True, seed=4)
-        res.append((obs, rew))
+    bf, bs = _bufs(full, n), _bufs(shard, per)
+    af, ash = full.empty(n, full.nu), shard.empty(per, shard.nu)
+    full.reset(bf[0], seed=4)
+    shard.reset(bs[0], seed=4)
+    full.clear_status()
+    idx = np.unique(np.linspace(0, n - 1, 64).round().astype(int))
+    ti = torch.from_numpy(idx).cuda()
+    q, v, w, p = full.empty(n, full.nq), full.empty(n, full.nv), full.empty(n, full.nv), full.empty(n, full.nparam)
+    oks, eqs, evs, misses, n_done = [], [], [], [], 0
+    for k in range(steps):
+        if k in C4_CHECK:
+            full.get_state(q, v, w, p)
+            pre = dict(qpos=q[ti].cpu().numpy().astype(np.float64), qvel=v[ti].cpu().numpy().astype(np.float64),
+                       warm=w[ti].cpu().numpy().astype(np.float64), params=p[ti].cpu().numpy().astype(np.float64))
+        full.random_actions(af, 9, k)
+        shard.random_actions(ash, 9, k)
+        full.step(af, *bf, autoreset=True, seed=4)
+        shard.step(ash, *bs, autoreset=True, seed=4)
+        for a, b in zip(bf[:3], bs[:3]):
+            assert torch.equal(a[3 * per:4 * per], b), f"shard differs from the full batch at step {k}"
+        n_done += int(bf[2].sum())
+        if k in C4_CHECK:
+            full.get_state(q, v)
+            dn = bf[2][ti].cpu().numpy()
+            sel = np.nonzero(dn == 0)[0]   # an env whose episode ended holds the new episode's state
+            a = af[ti].cpu().numpy().astype(np.float64)[sel]
+            st = {key: val[sel].copy() for key, val in pre.items()}
+            _, _, _, _, ost = o.step(st, a, nthreads=8)
+            assert not (np.bitwise_or.reduce(ost) & 24), "oracle dropped constraints at MuJoCo's caps"
+            qg, vg = q[ti].cpu().numpy()[sel], v[ti].cpu().numpy()[sel]
+            eq, ev, okk = _state_err(qg, vg, st["qpos"], st["qvel"])
+            oks.append(okk)
+            eqs.append(eq)
+            evs.append(ev)
+            misses += [(k, int(idx[sel[j]]), st["params"][j], st["qpos"][j], st["qvel"][j], st["warm"][j], a[j],
+                        qg[j].astype(np.float64), vg[j].astype(np.float64)) for j in np.where(~okk)[0]]
     torch.cuda.synchronize()
-    (of, rf), (os_, rs) = res
-    assert bool(torch.isfinite(of).all()) and bool(torch.isfinite(rf).all())
-    assert torch.equal(of[3 * per:4 * per], os_) and torch.equal(rf[3 * per:4 * per], rs)
+    assert bool(torch.isfinite(bf[0]).all()) and bool(torch.isfinite(bf[1]).all())
+    assert n_done >= n, f"the run crossed no horizon boundary ({n_done} episode ends)"
+    sticky = _sticky(full, n)
+    n_over = int(((sticky & _native.ST_OVERFLOW) != 0).sum())
+    ok = np.concatenate(oks)
+    label = f"config 4 {env_id} ({n} envs, {steps} steps, {len(C4_CHECK)} checked steps)"
+    print(f"{label}: {ok.mean():.4f} of {ok.size} teacher-forced cases within tolerance; {n_done} episode ends; "
+          f"envs dropping constraints: {n_over}")
+    _hard_cap(np.concatenate(eqs), np.concatenate(evs), label)
+    unexplained = _classify_misses(env_id, misses, label=label)
+    assert n_over == 0, n_over
+    assert ok.mean() >= ONE_STEP_MIN, ok.mean()
+    assert not unexplained, unexplained
