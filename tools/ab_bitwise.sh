@@ -1,5 +1,9 @@
+#!/bin/bash
+# Bitwise A/B of library variants (run through gpurun): bash tools/ab_bitwise.sh TAG variant...
+# Deterministic rollouts (tools/rollout_dump.py) of main and of each mj_envs_amd/libadroit_hip_<variant>.so
+# compared array for array, then tools/ab.sh under the random and DAPG policies.  Dumps stay in /tmp
+# on the box (they exceed gpurun_out's size cap); logs go to gpurun_out/TAG_*.
 set -e
-# usage: bash tools/_r06r.sh TAG variant...   (bitwise rollouts of each variant against main, then A/B)
 TAG=$1; shift
 timeout -k 10 120 python -u tools/rollout_dump.py /tmp/${TAG}_main.npz > gpurun_out/${TAG}_dump.log 2>&1
 for v in "$@"; do
