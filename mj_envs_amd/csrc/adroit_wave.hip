@@ -350,6 +350,9 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[Tree<TASK>:
   AW_PROF(s, PR_JT_TOUCH);
 }
 
+#ifndef AW_QPOS_COMP
+#define AW_QPOS_COMP 1
+#endif
 // mj_Euler: implicit joint damping (M + h D factored over the dof tree, aw_tree.h),
 // semi-implicit positions, warmstart <- qacc
 template <int TASK>
@@ -372,7 +375,18 @@ AW_DEV void euler(const DModel& m, Env& s, int lane, const float (&Mrow)[Tree<TA
   if (lane < NV) {
     float v = s.qvel[lane] + h * acc;
     s.qvel[lane] = v;
+#if AW_QPOS_COMP
+    // qpos += h v as MuJoCo's fp64 sum: qpos + qlo carries the position to ~2^-48 relative across the
+    // env-step's substeps (TwoProduct of h v, TwoSum into qpos, renormalised), so the fp64 consumers
+    // (qpos64) see the reference's positions at substeps 2.. instead of a rounding per substep
+    const float q = s.qpos[lane], p = h * v, pe = fmaf(h, v, -p);
+    const float sm = q + p, bb = sm - q, e = (q - (sm - bb)) + (p - bb);
+    const float lo = s.qlo[lane] + (pe + e), hi = sm + lo;
+    s.qpos[lane] = hi;
+    s.qlo[lane] = lo - (hi - sm);
+#else
     s.qpos[lane] += h * v;
+#endif
     s.warm[lane] = d.qacc;
   }
   wsync();
@@ -383,7 +397,8 @@ AW_DEV void euler(const DModel& m, Env& s, int lane, const float (&Mrow)[Tree<TA
 // reference's do_simulation writes ctrl once before its frame_skip mj_step calls
 template <int NV>
 AW_DEV void reset_state(Env& s, int lane) {
-  if (lane < NV) { s.qpos[lane] = 0.f; s.qvel[lane] = 0.f; s.warm[lane] = 0.f; s.ctrl[lane] = 0.f; }
+  if (lane < NV) { s.qpos[lane] = 0.f; s.qlo[lane] = 0.f; s.qvel[lane] = 0.f; s.warm[lane] = 0.f; }
+  if (lane < MAXU) s.ctrl[lane] = 0.f;
   wsync();
 }
 
@@ -416,6 +431,7 @@ template <int NV>
 AW_DEV void load_env(const DModel& m, Env& s, const DState& st, int env, int lane) {
   if (lane < NV) {
     s.qpos[lane] = st.qpos[(size_t)env * m.nq + lane];
+    s.qlo[lane] = 0.f;   // the stored state is fp32: the env-step starts from it exactly
     s.qvel[lane] = st.qvel[(size_t)env * m.nv + lane];
     s.warm[lane] = st.warm[(size_t)env * m.nv + lane];
   }
@@ -650,7 +666,8 @@ AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lan
   AW_PROF(s, PR_TASK);
   AW_PROF_COUNT(s, PR_CALLS);
   if (lane == 0)
-    for (int i = 0; i < AW_NPROF; i++) atomicAdd(&g_stage_prof[i], (unsigned long long)s.prof_acc[i]);
+    for (int i = 0; i < AW_NPROF; i++)
+      if (!prof_is_count(i)) atomicAdd(&g_stage_prof[i], (unsigned long long)s.prof_acc[prof_slot(i)]);
 #endif
 }
 
@@ -981,7 +998,7 @@ __global__ void __launch_bounds__(64) k_task_eval(DModel m, int n, const float* 
   __shared__ Env s;
   const int i = blockIdx.x, lane = threadIdx.x;
   if (i >= n) return;
-  if (lane < m.nq) s.qpos[lane] = qpos[(size_t)i * m.nq + lane];
+  if (lane < m.nq) { s.qpos[lane] = qpos[(size_t)i * m.nq + lane]; s.qlo[lane] = 0.f; }
   if (lane < m.nv) s.qvel[lane] = qvel[(size_t)i * m.nv + lane];
   for (int k = lane; k < m.nbody * 3; k += 64) (&s.xpos[0][0])[k] = xpos[(size_t)i * m.nbody * 3 + k];
   for (int k = lane; k < m.nbody * 4; k += 64) (&s.xquat[0][0])[k] = xquat[(size_t)i * m.nbody * 4 + k];
@@ -1080,7 +1097,7 @@ __global__ void __launch_bounds__(256) k_depth(DModel m, DState st, int n, CamRe
   const int env = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   if (env >= n) return;
   if (tid < 64) {
-    if (lane < NV) s.qpos[lane] = st.qpos[(size_t)env * m.nq + lane];
+    if (lane < NV) { s.qpos[lane] = st.qpos[(size_t)env * m.nq + lane]; s.qlo[lane] = 0.f; }
     wsync();
     stage_model(m, s, st.params + (size_t)env * m.nparam, lane);
     stage_kinematics(m, s, lane);

@@ -106,6 +106,9 @@ static_assert(EFC_CAP <= MAXEFC && MAXDENSE <= EFC_CAP, "constraint capacities")
 }  // inline namespace
 }  // namespace aw
 
+#ifdef AW_STAGE_PROF
+extern __device__ unsigned long long g_stage_prof[];   // adroit_wave.hip (stage profiler builds)
+#endif
 namespace aw {
 constexpr int JSPILL_FAST = (FAST_MAXDENSE_ALLOC - 32) * VS, JSPILL_WIDE = (WIDE_MAXDENSE - 32) * VS;
 #ifdef AW_WIDE
@@ -129,12 +132,22 @@ enum {
   PR_MPR_PAIRS, PR_MPR_CONTACTS   // counts: MPR pairs past the midphase, contacts they emitted
 };
 static_assert(PR_MPR_CONTACTS < AW_NPROF, "stage profiler ids");
+// Event counts (calls, substeps, iterations, rows, contacts, MPR pairs) go straight to the device
+// global (lane-0 atomics); only the timed stages keep a per-env 32-bit accumulator in LDS, at a
+// compact slot, so the profiling build's Env stays inside the product's 20 480-byte LDS granule.
+__host__ __device__ constexpr bool prof_is_count(int id) {
+  return (id >= PR_CALLS && id <= PR_NCON) || id == PR_NT_OFFD_ROWS || id >= PR_MPR_PAIRS;
+}
+__host__ __device__ constexpr int prof_slot(int id) { return id < PR_CALLS ? id : id < PR_NT_OFFD_ROWS ? id - 6 : id - 7; }
+constexpr int AW_NPROF_T = prof_slot(PR_CS_J) + 1;
+static_assert(prof_slot(PR_NT_INIT) == PR_CALLS && prof_slot(PR_CO_KIN64) == prof_slot(PR_NT_HOFFD) + 1 &&
+              !prof_is_count(PR_CS_J) && prof_is_count(PR_NT_OFFD_ROWS), "stage profiler slots");
 #ifdef AW_STAGE_PROF
 #define AW_PROF_START(S)                                            \
   do {                                                              \
     unsigned _t = (unsigned)__builtin_amdgcn_s_memtime();           \
     if (threadIdx.x == 0) {                                         \
-      for (int _i = 0; _i < AW_NPROF; _i++) (S).prof_acc[_i] = 0;   \
+      for (int _i = 0; _i < AW_NPROF_T; _i++) (S).prof_acc[_i] = 0; \
       (S).prof_t = _t;                                              \
     }                                                               \
   } while (0)
@@ -143,12 +156,12 @@ static_assert(PR_MPR_CONTACTS < AW_NPROF, "stage profiler ids");
     __syncthreads();                                                \
     unsigned _t = (unsigned)__builtin_amdgcn_s_memtime();           \
     if (threadIdx.x == 0) {                                         \
-      (S).prof_acc[ID] += _t - (S).prof_t;                          \
+      (S).prof_acc[prof_slot(ID)] += _t - (S).prof_t;               \
       (S).prof_t = _t;                                              \
     }                                                               \
   } while (0)
-#define AW_PROF_COUNT(S, ID) do { if (threadIdx.x == 0) (S).prof_acc[ID] += 1; } while (0)
-#define AW_PROF_ADD(S, ID, V) do { if (threadIdx.x == 0) (S).prof_acc[ID] += (unsigned)(V); } while (0)
+#define AW_PROF_COUNT(S, ID) do { if (threadIdx.x == 0) atomicAdd(&::g_stage_prof[ID], 1ull); } while (0)
+#define AW_PROF_ADD(S, ID, V) do { if (threadIdx.x == 0) atomicAdd(&::g_stage_prof[ID], (unsigned long long)(V)); } while (0)
 #elif defined(AW_TRACE)   // debugging builds: every stage boundary printed by lane 0 (device printf)
 #define AW_PROF_START(S) ((void)0)
 #define AW_PROF(S, ID) do { if (threadIdx.x == 0) printf("wg %d stage %d\n", (int)blockIdx.x, (int)(ID)); } while (0)
@@ -327,7 +340,8 @@ struct __attribute__((aligned(16))) Env {
     };
   };
   // persistent
-  float qpos[MAXV], qvel[MAXV], warm[MAXV], ctrl[MAXV];
+  float qpos[MAXV], qvel[MAXV], warm[MAXV], ctrl[MAXU];
+  float qlo[MAXV];          // qpos = qpos + qlo inside an env-step (mj_Euler's fp64 position sum; 0 at its start)
   float xpos[MAXB][3], xquat[MAXB][4];
   float sxpos[MAXS][3];
   float txmat[MAXTOUCH][9];
@@ -355,7 +369,7 @@ struct __attribute__((aligned(16))) Env {
 #ifdef AW_STAGE_PROF
   // 32-bit: one env-step's cycles per stage (summed into 64-bit globals after each env-step); keeps
   // the profiling build's Env inside k_step's 20 480-byte LDS granule, i.e. at the product's occupancy
-  unsigned prof_acc[AW_NPROF];
+  unsigned prof_acc[AW_NPROF_T];
   unsigned prof_t;
 #endif
 };
@@ -365,6 +379,9 @@ struct __attribute__((aligned(16))) Env {
 // its first MAXPAIR shorts hold the broadphase pair list
 constexpr int KIN64_OFF = MAXPAIR * 2;
 static_assert(KIN64_OFF % 16 == 0 && KIN64_OFF + MAXB * 8 * 8 <= JL * VS * 4, "fp64 frames do not fit in the dense-J rows");
+// joint position j in fp64: the env-step's compensated sum qpos + qlo (the fp64 consumers: frames of
+// the MPR / near-margin contact decisions, joint and tendon limit activation)
+AW_DEV double qpos64(const Env& s, int j) { return (double)s.qpos[j] + (double)s.qlo[j]; }
 AW_DEV double* kin64(Env& s, int b) {
   return reinterpret_cast<double*>(reinterpret_cast<char*>(&s.J[0][0]) + KIN64_OFF) + 8 * b;
 }

@@ -242,9 +242,9 @@ AW_DEV void stage_kin64(const DModel& m, Env& s, int lane) {
     const bool slide = MD(jnt_type, jl) == JNT_SLIDE;
     double sn = 0.0, cs = 1.0;
 #ifdef AW_OCML_SINCOS
-    if (!slide) sincos((double)s.qpos[jl] * 0.5, &sn, &cs);
+    if (!slide) sincos(qpos64(s, jl) * 0.5, &sn, &cs);
 #else
-    if (!slide) sincos64((double)s.qpos[jl] * 0.5, &sn, &cs);
+    if (!slide) sincos64(qpos64(s, jl) * 0.5, &sn, &cs);
 #endif
     const double p0 = MD(jnt_pos64, 3 * jl), p1 = MD(jnt_pos64, 3 * jl + 1), p2 = MD(jnt_pos64, 3 * jl + 2);
     SC[0] = sn;
@@ -279,7 +279,7 @@ AW_DEV void stage_kin64(const DModel& m, Env& s, int lane) {
         for (int c = 0; c < 3; c++) axis[c] = SCj[2 + c];
         const double kind = SCj[5];
         if (kind == 1.0) {
-          const double qj = (double)s.qpos[j];
+          const double qj = qpos64(s, j);
           double xaxis[3];
           rotvq(xaxis, axis, xq);
           for (int c = 0; c < 3; c++) xp[c] += xaxis[c] * qj;

@@ -280,7 +280,7 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
   int lo = 0, hi = 0;
   float dlo = 0, dhi = 0;
   if (lim && lane < m.njnt && MD(jnt_limited, lane)) {
-    const double q = (double)s.qpos[lane], mgd = MD(jnt_margin64, lane);
+    const double q = qpos64(s, lane), mgd = MD(jnt_margin64, lane);
     const double d0 = __dsub_rn(q, MD(jnt_range64, 2 * lane));
     const double d1 = __dsub_rn(MD(jnt_range64, 2 * lane + 1), q);
     lo = d0 < mgd; hi = d1 < mgd;
@@ -303,8 +303,8 @@ AW_DEV void stage_constraints(const DModel& m, Env& s, int lane) {
   if (lim && lane < m.ntendon && MD(ten_limited, lane)) {
     const int d1 = MD(ten_d1, lane);
     // fixed tendon length in fp64 with the reference's operation order (no contraction)
-    const double len = __dadd_rn(__dmul_rn(MD(ten_c0_64, lane), (double)s.qpos[MD(ten_d0, lane)]),
-                                 d1 >= 0 ? __dmul_rn(MD(ten_c1_64, lane), (double)s.qpos[d1]) : 0.0);
+    const double len = __dadd_rn(__dmul_rn(MD(ten_c0_64, lane), qpos64(s, MD(ten_d0, lane))),
+                                 d1 >= 0 ? __dmul_rn(MD(ten_c1_64, lane), qpos64(s, d1)) : 0.0);
     const double mgd = MD(ten_margin64, lane);
     const double e0 = __dsub_rn(len, MD(ten_range64, 2 * lane));
     const double e1 = __dsub_rn(MD(ten_range64, 2 * lane + 1), len);

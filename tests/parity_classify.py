@@ -93,6 +93,7 @@ class Ctx:
         m1 = load_task_model(env_id, variation)
         m1.dims["task_frame_skip"] = 1
         self.one = _native.Sim(m1.to_blob(), 1)
+        self._fs, self.fault = {1: self.one}, (0, 0)   # frame_skip-k handles (gpu_substeps)
         self.torch = torch
         A = self.m.arrays
         g1 = list(np.asarray(A["pair_geom1"], int)) + list(np.asarray(A["cand_geom1"], int))
@@ -151,15 +152,35 @@ class Ctx:
                 self.o.set_margin_nudge()
         return q, v, w
 
-    def gpu_substep(self, params, q, v, w, act):
-        """one GPU mj_step from (q, v, w) through the frame_skip-1 handle"""
-        one, torch = self.one, self.torch
-        ob, rw = one.empty(1, one.obs_dim), one.empty(1)
-        dn, gl = one.empty(1, dtype=torch.uint8), one.empty(1, dtype=torch.uint8)
-        qq, vv, ww = one.empty(1, one.nq), one.empty(1, one.nv), one.empty(1, one.nv)
-        one.set_state(self._t(q[None]), self._t(v[None]), self._t(w[None]), self._t(np.asarray(params)[None]))
-        one.step(self._t(np.asarray(act)[None]), ob, rw, dn, gl)
-        one.get_state(qq, vv, ww)
+    def set_fault(self, kind, arg):
+        """aw_set_fault on every GPU handle of the context (the classifier inspects the faulty kernel)"""
+        self.fault = (kind, arg)
+        for h in self._fs.values():
+            h.set_fault(kind, arg)
+
+    def _fs_handle(self, k):
+        h = self._fs.get(k)
+        if h is None:
+            from mj_envs_amd import _native
+            mk = load_task_model(self.env_id, self.variation)
+            mk.dims["task_frame_skip"] = k
+            h = self._fs[k] = _native.Sim(mk.to_blob(), 1)
+            if self.fault != (0, 0):
+                h.set_fault(*self.fault)
+        return h
+
+    def gpu_substeps(self, params, q, v, w, act, k):
+        """the GPU's state after the first k substeps of the env-step from (q, v, w): the env-step of a
+        frame_skip-k handle is exactly those substeps.  (Inside an env-step the kernel carries each
+        position as qpos + qlo across substeps, so k separate one-substep env-steps from the rounded
+        fp32 states would not reproduce it.)"""
+        h, torch = self._fs_handle(k), self.torch
+        ob, rw = h.empty(1, h.obs_dim), h.empty(1)
+        dn, gl = h.empty(1, dtype=torch.uint8), h.empty(1, dtype=torch.uint8)
+        qq, vv, ww = h.empty(1, h.nq), h.empty(1, h.nv), h.empty(1, h.nv)
+        h.set_state(self._t(q[None]), self._t(v[None]), self._t(w[None]), self._t(np.asarray(params)[None]))
+        h.step(self._t(np.asarray(act)[None]), ob, rw, dn, gl)
+        h.get_state(qq, vv, ww)
         torch.cuda.synchronize()
         return tuple(x[0].cpu().numpy().astype(np.float64) for x in (qq, vv, ww))
 
@@ -421,11 +442,12 @@ def shadowed(ctx, params, qpos, qvel, warm, act, gpu, jar_log=None):
     """(c): "shadowed", "switch" (a switch on the GPU's own trajectory), False (a contradiction there)
     or None; with the reason"""
     ctrl = ctx.ctrl(act)
-    q, v, w = (f32(x) for x in (qpos, qvel, warm))
+    q0, v0, w0 = (f32(x) for x in (qpos, qvel, warm))
+    q, v, w = q0, v0, w0
     worst = 0.0
     for j in range(ctx.frame_skip):
         qs, vs, ws = q.copy(), v.copy(), w.copy()
-        q, v, w = ctx.gpu_substep(params, qs, vs, ws, act)
+        q, v, w = ctx.gpu_substeps(params, q0, v0, w0, act, j + 1)
         qo, vo, _ = ctx.oracle_steps(params, qs, vs, ws, ctrl, 1)
         eq = np.abs(q - qo) / (2e-5 + 1e-5 * np.abs(qo))
         ev = np.abs(v - vo) / (5e-3 * (1 + np.abs(vo)))

@@ -87,12 +87,12 @@ def _faulty_run(env_id, kind, arg, n, warm_steps, steps, policy):
 def _classify_with_fault(env_id, misses, kind, arg):
     from parity_classify import classify_misses, context
     ctx = context(env_id)
-    ctx.one.set_fault(kind, arg)        # the classifier inspects the faulty kernel
+    ctx.set_fault(kind, arg)        # the classifier inspects the faulty kernel
     try:
         sample = [misses[i] for i in np.unique(np.linspace(0, len(misses) - 1, MAX_CLASSIFIED).round().astype(int))]
         unexplained, tally = classify_misses(env_id, sample, label=f"fault {kind}/{arg}")
     finally:
-        ctx.one.set_fault(0, 0)
+        ctx.set_fault(0, 0)
     return sample, unexplained, tally
 
 
