@@ -397,8 +397,7 @@ AW_DEV void euler(const DModel& m, Env& s, int lane, const float (&Mrow)[Tree<TA
 // reference's do_simulation writes ctrl once before its frame_skip mj_step calls
 template <int NV>
 AW_DEV void reset_state(Env& s, int lane) {
-  if (lane < NV) { s.qpos[lane] = 0.f; s.qlo[lane] = 0.f; s.qvel[lane] = 0.f; s.warm[lane] = 0.f; }
-  if (lane < MAXU) s.ctrl[lane] = 0.f;
+  if (lane < NV) { s.qpos[lane] = 0.f; s.qlo[lane] = 0.f; s.qvel[lane] = 0.f; s.warm[lane] = 0.f; s.ctrl[lane] = 0.f; }
   wsync();
 }
 
@@ -667,7 +666,7 @@ AW_DEV void env_step(const DModel& m, Env& s, const DState& st, int env, int lan
   AW_PROF_COUNT(s, PR_CALLS);
   if (lane == 0)
     for (int i = 0; i < AW_NPROF; i++)
-      if (!prof_is_count(i)) atomicAdd(&g_stage_prof[i], (unsigned long long)s.prof_acc[prof_slot(i)]);
+      if (!prof_global(i)) atomicAdd(&g_stage_prof[i], (unsigned long long)s.prof_acc[prof_slot(i)]);
 #endif
 }
 

@@ -132,16 +132,24 @@ enum {
   PR_MPR_PAIRS, PR_MPR_CONTACTS   // counts: MPR pairs past the midphase, contacts they emitted
 };
 static_assert(PR_MPR_CONTACTS < AW_NPROF, "stage profiler ids");
-// Event counts (calls, substeps, iterations, rows, contacts, MPR pairs) go straight to the device
-// global (lane-0 atomics); only the timed stages keep a per-env 32-bit accumulator in LDS, at a
-// compact slot, so the profiling build's Env stays inside the product's 20 480-byte LDS granule.
+// Event counts (calls, substeps, iterations, rows, contacts, MPR pairs) and the stages timed once
+// per env-step or cheap (pre, task, reset, checks, plane / sphere colliders) go straight to the
+// device global (lane-0 atomics); the other timed stages keep a per-env 32-bit accumulator in LDS at
+// a compact slot, so the profiling build's Env stays inside the product's 20 480-byte LDS granule.
 __host__ __device__ constexpr bool prof_is_count(int id) {
   return (id >= PR_CALLS && id <= PR_NCON) || id == PR_NT_OFFD_ROWS || id >= PR_MPR_PAIRS;
 }
-__host__ __device__ constexpr int prof_slot(int id) { return id < PR_CALLS ? id : id < PR_NT_OFFD_ROWS ? id - 6 : id - 7; }
-constexpr int AW_NPROF_T = prof_slot(PR_CS_J) + 1;
-static_assert(prof_slot(PR_NT_INIT) == PR_CALLS && prof_slot(PR_CO_KIN64) == prof_slot(PR_NT_HOFFD) + 1 &&
-              !prof_is_count(PR_CS_J) && prof_is_count(PR_NT_OFFD_ROWS), "stage profiler slots");
+__host__ __device__ constexpr bool prof_global(int id) {
+  return prof_is_count(id) || id == PR_PRE || id == PR_TASK || id == PR_RESET || id == PR_CHECK || id == PR_CO_C0 ||
+         id == PR_CO_C1;
+}
+__host__ __device__ constexpr int prof_slot(int id) {
+  int k = 0;
+  for (int i = 0; i < id; i++) k += prof_global(i) ? 0 : 1;
+  return k;
+}
+constexpr int AW_NPROF_T = prof_slot(AW_NPROF);
+static_assert(AW_NPROF_T == 29, "stage profiler slots");
 #ifdef AW_STAGE_PROF
 #define AW_PROF_START(S)                                            \
   do {                                                              \
@@ -156,7 +164,10 @@ static_assert(prof_slot(PR_NT_INIT) == PR_CALLS && prof_slot(PR_CO_KIN64) == pro
     __syncthreads();                                                \
     unsigned _t = (unsigned)__builtin_amdgcn_s_memtime();           \
     if (threadIdx.x == 0) {                                         \
-      (S).prof_acc[prof_slot(ID)] += _t - (S).prof_t;               \
+      if (prof_global(ID))                                          \
+        atomicAdd(&::g_stage_prof[ID], (unsigned long long)(_t - (S).prof_t)); \
+      else                                                          \
+        (S).prof_acc[prof_slot(ID)] += _t - (S).prof_t;             \
       (S).prof_t = _t;                                              \
     }                                                               \
   } while (0)
@@ -340,7 +351,7 @@ struct __attribute__((aligned(16))) Env {
     };
   };
   // persistent
-  float qpos[MAXV], qvel[MAXV], warm[MAXV], ctrl[MAXU];
+  float qpos[MAXV], qvel[MAXV], warm[MAXV], ctrl[MAXV];
   float qlo[MAXV];          // qpos = qpos + qlo inside an env-step (mj_Euler's fp64 position sum; 0 at its start)
   float xpos[MAXB][3], xquat[MAXB][4];
   float sxpos[MAXS][3];
@@ -374,6 +385,12 @@ struct __attribute__((aligned(16))) Env {
 #endif
 };
 
+// The persistent arrays start on 16-byte boundaries.  A layout that put them at 8 mod 16 (ctrl sized
+// by MAXU, r06 bisection: tools/diag_tiers.py) made the fast and the wide tier diverge bitwise in
+// hammer's free-object dofs after a few env-steps -- an alignment-phase dependence not root-caused
+// (DESIGN.md §7); held here so no layout change reintroduces it unnoticed.
+static_assert(offsetof(Env, xpos) % 16 == 0 && offsetof(Env, xquat) % 16 == 0 && offsetof(Env, gsize) % 16 == 0,
+              "persistent Env arrays must keep their 16-byte alignment phase");
 // fp64 body frames of the MPR (cylinder) geometry, stage_kin64 -> narrowphase: [MAXB][8] doubles
 // (xpos[3], xquat[4], pad) in the dense-J storage, dead from kinematics until the constraint rows;
 // its first MAXPAIR shorts hold the broadphase pair list
@@ -381,7 +398,10 @@ constexpr int KIN64_OFF = MAXPAIR * 2;
 static_assert(KIN64_OFF % 16 == 0 && KIN64_OFF + MAXB * 8 * 8 <= JL * VS * 4, "fp64 frames do not fit in the dense-J rows");
 // joint position j in fp64: the env-step's compensated sum qpos + qlo (the fp64 consumers: frames of
 // the MPR / near-margin contact decisions, joint and tendon limit activation)
-AW_DEV double qpos64(const Env& s, int j) { return (double)s.qpos[j] + (double)s.qlo[j]; }
+#ifndef AW_QPOS64_LO
+#define AW_QPOS64_LO 1
+#endif
+AW_DEV double qpos64(const Env& s, int j) { return (double)s.qpos[j] + (AW_QPOS64_LO ? (double)s.qlo[j] : 0.0); }
 AW_DEV double* kin64(Env& s, int b) {
   return reinterpret_cast<double*>(reinterpret_cast<char*>(&s.J[0][0]) + KIN64_OFF) + 8 * b;
 }
