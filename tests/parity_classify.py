@@ -215,6 +215,13 @@ POS_TOL, DIST_TOL = 1e-4, 1e-5   # matched contacts: a point 0.1 mm or a depth 1
 TIE_DRAWS, TIE_ULPS = 8, 16
 
 
+def perturb_qpos(q, eps, rng):
+    """qpos moved by up to eps (TIE_ULPS fp32 ulps) of max(|q|, 1) per joint: the fp32 resolution of
+    the kinematic chain, whose rounding is absolute (~ulp of the O(1) frame entries) however small the
+    joint angle -- a purely relative perturbation of a joint near 0 rad would be far below it"""
+    return q + eps * np.maximum(np.abs(q), 1.0) * rng.uniform(-1, 1, q.shape)
+
+
 def _pair_contacts_oracle(ctx, key, params, q, v, w, ctrl):
     ctx.o.forward1(params, q, v, w, ctrl)
     oc = ctx.o.get("contact").reshape(-1, 23)
@@ -231,14 +238,14 @@ def _lists_differ(a, b):
 def oracle_tie(ctx, key, params, q, v, w, ctrl, seed=0):
     """Is the reference's own collider decision for this pair unstable at fp32 resolution?  True when
     the oracle's contacts of the pair change (count, a point by > POS_TOL or a depth by > DIST_TOL)
-    under <= TIE_ULPS-ulp perturbations of qpos (TIE_DRAWS draws): a degenerate configuration (a
+    under <= TIE_ULPS-ulp perturbations of qpos (perturb_qpos, TIE_DRAWS draws): a degenerate configuration (a
     capsule parallel to a face, a flat minimum of the segment-box distance, a cylinder's line contact)
     whose tie is broken by rounding."""
     base = _pair_contacts_oracle(ctx, key, params, q, v, w, ctrl)
     rng = np.random.default_rng(seed)
     eps = TIE_ULPS * 2.0 ** -23
     for _ in range(TIE_DRAWS):
-        qp = q * (1 + eps * rng.uniform(-1, 1, q.shape))
+        qp = perturb_qpos(q, eps, rng)
         if _lists_differ(_pair_contacts_oracle(ctx, key, params, qp, v, w, ctrl), base):
             return True
     return False
@@ -384,7 +391,8 @@ def tie_causal(ctx, params, q, v, w, ctrl, nsub, gpu, trials=8, ulps=16, seed=0)
     eps = ulps * 2.0 ** -23
     sq = sv = 0.0
     for _ in range(trials):
-        pq, pv, pw = (x * (1 + eps * rng.uniform(-1, 1, x.shape)) for x in (q, v, w))
+        pq = perturb_qpos(q, eps, rng)
+        pv, pw = (x * (1 + eps * rng.uniform(-1, 1, x.shape)) for x in (v, w))
         nq, nv_, _ = ctx.oracle_steps(params, pq, pv, pw, ctrl, nsub)
         if within_tol(gq, gv, nq, nv_):
             return True, 0.0

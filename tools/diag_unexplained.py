@@ -55,6 +55,8 @@ def main(paths):
             P, q, v, w, act = (z[k][i] for k in ("params", "qpos", "qvel", "warm", "act"))
             ctrl = ctx.ctrl(act)
             print(f"--- step {int(z['step'][i])} env {int(z['env'][i])}")
+            gpu_traj = os.environ.get("AW_DIAG_GPU_TRAJ") == "1"   # walk the GPU's own substeps instead
+            q0, v0, w0 = q.copy(), v.copy(), w.copy()
             for j in range(ctx.frame_skip):
                 d = ctx.gpu_forward(P, q, v, w, ctrl)
                 orc = ctx.oracle_forward(P, q, v, w, ctrl)
@@ -71,7 +73,11 @@ def main(paths):
                 nefc_o = int(orc["scalars"][1])
                 rows_diff = d["nefc"] == nefc_o and (gst != ost).any()
                 if not diff_pairs and d["nefc"] == nefc_o and not rows_diff:
-                    q, v, w = ctx.oracle_steps(P, q, v, w, ctrl, 1)
+                    if gpu_traj:
+                        q, v, w = ctx.gpu_substeps(P, q0.astype(np.float32).astype(np.float64), v0.astype(np.float32).astype(np.float64),
+                                                   w0.astype(np.float32).astype(np.float64), act, j + 1)
+                    else:
+                        q, v, w = ctx.oracle_steps(P, q, v, w, ctrl, 1)
                     continue
                 print(f"  substep {j}: ncon GPU {d['ncon']} / oracle {int(orc['scalars'][0])}, nefc {d['nefc']} / "
                       f"{nefc_o}, Newton GPU {d['solver_iter']} it ({d['solver_exit']}) / oracle {int(orc['scalars'][2])} it")
