@@ -251,6 +251,50 @@ def oracle_tie(ctx, key, params, q, v, w, ctrl, seed=0):
     return False
 
 
+POSE_TOL = 1e-5   # body frames: the GPU's fp32 kinematics against the reference's fp64 (m, quaternion units)
+
+
+def _quat2mat(qt):
+    w, x, y, z = np.asarray(qt, float) / np.linalg.norm(qt)
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def pose_tie(ctx, key, d, gl, params, q, v, w, ctrl):
+    """Is the GPU's contact list for this pair the REFERENCE's own collider output on the GPU's body
+    frames?  True when the two bodies' GPU frames (fp32 kinematics) agree with the reference's to
+    POSE_TOL and the oracle's collider, run on the geom poses composed from those frames, reproduces
+    the GPU's contacts: the difference is then the reference's decision flipping under an fp32-sized
+    pose change (a capsule parallel to a face, a segment inside a box), not a collider difference."""
+    A = ctx.m.arrays
+    gb = np.asarray(A["geom_bodyid"], int)
+    gp = np.asarray(A["geom_pos"], float).reshape(-1, 3)
+    gq = np.asarray(A["geom_quat"], float).reshape(-1, 4)
+    gs = np.asarray(A["geom_size"], float).reshape(-1, 3)
+    xp = np.asarray(d["xpos"], float).reshape(-1, 3)
+    xq = np.asarray(d["xquat"], float).reshape(-1, 4)
+    ctx.o.forward1(params, q, v, w, ctrl)
+    oxp, oxq = ctx.o.get("xpos").reshape(-1, 3), ctx.o.get("xquat").reshape(-1, 4)
+    for g in key:
+        b = gb[g]
+        if np.abs(xp[b] - oxp[b]).max() > POSE_TOL or np.abs(xq[b] - oxq[b]).max() > POSE_TOL:
+            return False
+    a, b = key
+    if ctx.gtype[a] > ctx.gtype[b]:
+        a, b = b, a
+
+    def pose(g):
+        R = _quat2mat(xq[gb[g]])
+        return xp[gb[g]] + R @ gp[g], (R @ _quat2mat(gq[g])).reshape(9)
+
+    (pa, ma), (pb, mb) = pose(a), pose(b)
+    ro = ctx.o.collide(ctx.gtype[a], pa, ma, gs[a], ctx.gtype[b], pb, mb, gs[b], ctx.margin_of[key][0])
+    lst = [(float(r[0]), np.asarray(r[1:4], float)) for r in ro]
+    return len(lst) == len(gl) and not _lists_differ(sorted(lst, key=lambda t: tuple(t[1])),
+                                                    sorted(gl, key=lambda t: tuple(t[1])))
+
+
 def forward_diff(ctx, params, q, v, w, ctrl, jar_log=None):
     """Compare the two forwards from the identical fp32 state (q, v, w rounded to fp32 for BOTH sides,
     as the GPU holds it).  Returns
@@ -282,9 +326,14 @@ def forward_diff(ctx, params, q, v, w, ctrl, jar_log=None):
             # reference itself breaks differently at fp32 resolution can excuse that
             why = (f"{far[0][0]}-only contact {name} at {far[0][1] - (mg or 0):+.2e} from its margin" if far else
                    f"contacts of {name} differ in point / depth")
-            if not oracle_tie(ctx, key, params, q, v, w, ctrl):
-                return "contradiction", why + " (the reference's decision is stable under 16-ulp perturbations)"
-            ties.append(dict(kind="tie", pair=key, name=name, why=why))
+            if oracle_tie(ctx, key, params, q, v, w, ctrl):
+                ties.append(dict(kind="tie", pair=key, name=name, why=why, pose=False))
+            elif pose_tie(ctx, key, d, gl, params, q, v, w, ctrl):
+                ties.append(dict(kind="tie", pair=key, name=name, why=why + " (the reference's collider on the GPU's "
+                                 "frames gives the GPU's contacts)", pose=True))
+            else:
+                return "contradiction", why + (" (the reference's decision is stable under 16-ulp perturbations and "
+                                               "its collider on the GPU's frames does not give the GPU's contacts)")
             continue
         for side, lst in (("gpu", gu), ("oracle", ou)):
             for dist, pos in lst:
@@ -433,6 +482,9 @@ def switch_event(ctx, params, q, v, w, act, gpu, jar_log=None):
         label = f"collider tie ({tie_recs[0]['name']})"
         if ok:
             return True, label, ratio
+        if all(r.get("pose") for r in tie_recs):
+            # proven on the GPU's own frames (pose_tie); what it may excuse is bounded by the class cap
+            return True, label + " [pose]", None
         notes.append(f"{label}: does not account for the GPU (ratio {ratio:.1f})")
     if contact_recs:
         ok, ratio = causal(ctx, params, q0, v0, w0, ctrl, ctx.frame_skip, gpu, contact_recs)
@@ -447,7 +499,7 @@ def switch_event(ctx, params, q, v, w, act, gpu, jar_log=None):
 
 
 def shadowed(ctx, params, qpos, qvel, warm, act, gpu, jar_log=None):
-    """(c): "shadowed", "switch" (a switch on the GPU's own trajectory), False (a contradiction there)
+    """(c): "shadowed", "switch" / "tie" (a switch / collider tie on the GPU's own trajectory), False (a contradiction there)
     or None; with the reason"""
     ctrl = ctx.ctrl(act)
     q0, v0, w0 = (f32(x) for x in (qpos, qvel, warm))
@@ -471,13 +523,13 @@ def shadowed(ctx, params, qpos, qvel, warm, act, gpu, jar_log=None):
             trec = [r for r in info if r["kind"] == "tie"]
             if trec:
                 ok, ratio = tie_causal(ctx, params, qs, vs, ws, ctrl, 1, (q, v))
-                if not ok:
+                if not ok and not all(r.get("pose") for r in trec):
                     return None, f"{why}; the tie ({trec[0]['name']}) does not account for it (ratio {ratio:.1f})"
             elif crec:
                 ok, ratio = causal(ctx, params, qs, vs, ws, ctrl, 1, (q, v), crec)
                 if not ok:
                     return None, f"{why}; the switch ({crec[0]['name']}) does not account for it (ratio {ratio:.1f})"
-            return "switch", f"{why}; at that state: {info[0]['name']}"
+            return ("tie" if trec else "switch"), f"{why}; at that state: {info[0]['name']}"
         worst = max(worst, loc)
     same = np.array_equal(q.astype(np.float32), np.asarray(gpu[0], np.float32)) and \
         np.array_equal(v.astype(np.float32), np.asarray(gpu[1], np.float32))
@@ -618,6 +670,8 @@ def classify_miss(env_id, ms, variation=None, jar_log=None):
         return "oracle-shadowed trajectory", why, None, dev
     if sh == "switch":
         return "switch on the GPU's own trajectory", why, None, dev
+    if sh == "tie":
+        return "collider tie on the GPU's own trajectory", why, None, dev
     ok, ratio = fp32_sensitive(ctx, params, q, v, w, a, gpu)
     if ok:
         return "fp32-sensitive reference", f"ratio {ratio:.2f}", ratio, dev
