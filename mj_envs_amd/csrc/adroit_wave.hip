@@ -350,9 +350,6 @@ AW_DEV void forward(const DModel& m, Env& s, int lane, float (&Mrow)[Tree<TASK>:
   AW_PROF(s, PR_JT_TOUCH);
 }
 
-#ifndef AW_QPOS_COMP
-#define AW_QPOS_COMP 1
-#endif
 // mj_Euler: implicit joint damping (M + h D factored over the dof tree, aw_tree.h),
 // semi-implicit positions, warmstart <- qacc
 template <int TASK>

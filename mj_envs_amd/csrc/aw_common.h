@@ -398,10 +398,20 @@ constexpr int KIN64_OFF = MAXPAIR * 2;
 static_assert(KIN64_OFF % 16 == 0 && KIN64_OFF + MAXB * 8 * 8 <= JL * VS * 4, "fp64 frames do not fit in the dense-J rows");
 // joint position j in fp64: the env-step's compensated sum qpos + qlo (the fp64 consumers: frames of
 // the MPR / near-margin contact decisions, joint and tendon limit activation)
-#ifndef AW_QPOS64_LO
-#define AW_QPOS64_LO 1
+// AW_QPOS_COMP (default 0): carry qpos + qlo across the substeps (adroit_wave.hip euler).  Measured
+// r06x / r06z: DAPG headline misses 41 -> 13 of 20 480 (0.99937); off by default because one relocate
+// config-3 wide-tier env-step then meets a capsule-box point choice the classifier cannot yet prove a
+// tie.
+#ifndef AW_QPOS_COMP
+#define AW_QPOS_COMP 0
 #endif
-AW_DEV double qpos64(const Env& s, int j) { return (double)s.qpos[j] + (AW_QPOS64_LO ? (double)s.qlo[j] : 0.0); }
+AW_DEV double qpos64(const Env& s, int j) {
+#if AW_QPOS_COMP
+  return (double)s.qpos[j] + (double)s.qlo[j];
+#else
+  return (double)s.qpos[j];
+#endif
+}
 AW_DEV double* kin64(Env& s, int b) {
   return reinterpret_cast<double*>(reinterpret_cast<char*>(&s.J[0][0]) + KIN64_OFF) + 8 * b;
 }

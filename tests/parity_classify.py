@@ -295,6 +295,32 @@ def pose_tie(ctx, key, d, gl, params, q, v, w, ctrl):
                                                     sorted(gl, key=lambda t: tuple(t[1])))
 
 
+def depth_tie(ctx, key, gl, ol, params, q, v, w, ctrl):
+    """Capsule-box with the same contact count and depths: is every GPU contact point an exact minimiser
+    of the REFERENCE's own capsule-box distance?  Each GPU point is projected on the capsule axis (the
+    reference's frames) and the reference's sphere-box collider at that axis point must give the same
+    depth (DIST_TOL): the GPU picked another point of a flat minimum (a capsule parallel to a face, a
+    segment inside the box), where the order of equal candidates is decided by rounding."""
+    a, b = key
+    if sorted((ctx.gtype[a], ctx.gtype[b])) != [3, 6] or len(gl) != len(ol) or not gl:
+        return False
+    if any(abs(x[0] - y[0]) > DIST_TOL for x, y in zip(sorted(gl, key=lambda t: t[0]), sorted(ol, key=lambda t: t[0]))):
+        return False
+    c, x = (a, b) if ctx.gtype[a] == 3 else (b, a)
+    ctx.o.forward1(params, q, v, w, ctrl)
+    gxp, gxm = ctx.o.get("geom_xpos").reshape(-1, 3), ctx.o.get("geom_xmat").reshape(-1, 9)
+    gs = np.asarray(ctx.m.arrays["geom_size"], float).reshape(-1, 3)
+    axis = gxm[c].reshape(3, 3)[:, 2]
+    mg = ctx.margin_of[key][0]
+    for dist, pos in gl:
+        t = float(np.clip(np.dot(pos - gxp[c], axis), -gs[c][1], gs[c][1]))
+        r = ctx.o.collide(2, gxp[c] + t * axis, np.eye(3).reshape(9), np.array([gs[c][0], 0.0, 0.0]),
+                          6, gxp[x], gxm[x], gs[x], mg)
+        if len(r) == 0 or abs(float(np.min(r[:, 0])) - dist) > DIST_TOL:
+            return False
+    return True
+
+
 def forward_diff(ctx, params, q, v, w, ctrl, jar_log=None):
     """Compare the two forwards from the identical fp32 state (q, v, w rounded to fp32 for BOTH sides,
     as the GPU holds it).  Returns
@@ -331,9 +357,13 @@ def forward_diff(ctx, params, q, v, w, ctrl, jar_log=None):
             elif pose_tie(ctx, key, d, gl, params, q, v, w, ctrl):
                 ties.append(dict(kind="tie", pair=key, name=name, why=why + " (the reference's collider on the GPU's "
                                  "frames gives the GPU's contacts)", pose=True))
+            elif not far and depth_tie(ctx, key, gl, ol, params, q, v, w, ctrl):
+                ties.append(dict(kind="tie", pair=key, name=name, why=why + " (every GPU point is an equal-depth "
+                                 "minimiser of the reference's distance)", pose=True))
             else:
-                return "contradiction", why + (" (the reference's decision is stable under 16-ulp perturbations and "
-                                               "its collider on the GPU's frames does not give the GPU's contacts)")
+                return "contradiction", why + (" (the reference's decision is stable under 16-ulp perturbations, its "
+                                               "collider on the GPU's frames does not give the GPU's contacts and "
+                                               "they are not equal-depth minimisers of its distance)")
             continue
         for side, lst in (("gpu", gu), ("oracle", ou)):
             for dist, pos in lst:
